@@ -1,0 +1,156 @@
+"""Synthetic sparse patterns (host-side input generation, numpy).
+
+Two families:
+
+* Exact rebuilds of SuiteSparse matrices that appear in the reference's published logs and are
+  defined by a formula (Trefethen_20000/20000b, mycielskian14/15/16). They reproduce what the
+  reference loader (Matrix.cpp:398-480) builds from the SuiteSparse ``.mtx`` files: symmetric
+  files store the lower triangle only and the loader does not mirror it, entries are listed
+  column by column, so every CSR row holds its lower-triangle columns in ascending order.
+* Seeded stand-ins for the BASELINE.json configs whose files are absent:
+  nips_like, cop20k_A_like, reddit_like, dlmc_like.
+
+All return (M, N, rowptr uint32[M+1], colidx uint32[nnz]).
+"""
+import numpy as np
+
+
+def _csr_from_coo(M, N, rows, cols):
+    rows = np.asarray(rows, dtype=np.int64)
+    cols = np.asarray(cols, dtype=np.int64)
+    order = np.lexsort((cols, rows))
+    rows = rows[order]
+    cols = cols[order]
+    rowptr = np.zeros(M + 1, dtype=np.int64)
+    np.add.at(rowptr, rows + 1, 1)
+    rowptr = np.cumsum(rowptr)
+    return M, N, rowptr.astype(np.uint32), cols.astype(np.uint32)
+
+
+def trefethen(n):
+    """Trefethen_<n>: primes on the diagonal, ones where |i-j| is a power of two (lower triangle)."""
+    rows = [np.arange(n)]
+    cols = [np.arange(n)]
+    p = 1
+    while p < n:
+        r = np.arange(p, n)
+        rows.append(r)
+        cols.append(r - p)
+        p <<= 1
+    return _csr_from_coo(n, n, np.concatenate(rows), np.concatenate(cols))
+
+
+def mycielskian(k):
+    """mycielskian<k>: A_{j+1} = [A A 0; A 0 e; 0 e' 0] from A_2 = K_2; lower triangle stored."""
+    n = 2
+    ei = np.array([1], dtype=np.int64)  # edges as (i > j)
+    ej = np.array([0], dtype=np.int64)
+    for _ in range(k - 2):
+        # v_i ~ u_j and v_j ~ u_i for each edge (i, j); u_i ~ w
+        ni = np.concatenate([ei, n + ej, n + ei, np.full(n, 2 * n)])
+        nj = np.concatenate([ej, ei, ej, n + np.arange(n)])
+        ei = np.maximum(ni, nj)
+        ej = np.minimum(ni, nj)
+        n = 2 * n + 1
+    return _csr_from_coo(n, n, ei, ej)
+
+
+SUITESPARSE_REBUILDS = {
+    "Trefethen_20000": lambda: trefethen(20000),
+    "Trefethen_20000b": lambda: trefethen(19999),
+    "mycielskian14": lambda: mycielskian(14),
+    "mycielskian15": lambda: mycielskian(15),
+    "mycielskian16": lambda: mycielskian(16),
+}
+
+
+def random_rows(M, N, nnz_per_row, seed, zipf=None, empty_frac=0.0):
+    """Rows with (roughly) nnz_per_row distinct columns; Zipf-popular columns when zipf is set."""
+    rng = np.random.default_rng(seed)
+    if np.isscalar(nnz_per_row):
+        counts = rng.poisson(nnz_per_row, size=M).clip(1, N)
+    else:
+        counts = np.asarray(nnz_per_row)
+    if empty_frac > 0:
+        counts[rng.random(M) < empty_frac] = 0
+    if zipf is not None:
+        w = 1.0 / np.arange(1, N + 1) ** zipf
+        w /= w.sum()
+        perm = rng.permutation(N)
+    rows, cols = [], []
+    for r in range(M):
+        c = int(counts[r])
+        if c == 0:
+            continue
+        if zipf is not None:
+            pick = rng.choice(N, size=min(N, int(c * 1.3) + 8), replace=True, p=w)
+            pick = np.unique(perm[pick])[:c]
+        else:
+            pick = rng.choice(N, size=c, replace=False)
+        rows.append(np.full(len(pick), r))
+        cols.append(pick)
+    return _csr_from_coo(M, N, np.concatenate(rows), np.concatenate(cols))
+
+
+def nips_like(seed=20250801):
+    """C1/C2 stand-in: 1,500 x 12,419, ~746k nnz, Zipf(1.1) column popularity."""
+    M, N, target = 1500, 12419, 746316
+    rng = np.random.default_rng(seed)
+    # ragged document lengths around 497 words
+    lens = rng.lognormal(mean=np.log(440), sigma=0.5, size=M)
+    lens = np.maximum(8, lens * (target / lens.sum())).astype(np.int64)
+    lens[: target - lens.sum()] += 1 if target > lens.sum() else 0
+    return random_rows(M, N, lens, seed + 1, zipf=1.1)
+
+
+def banded_fem_like(n, nnz_per_row, seed, band=64):
+    """cop20k_A-like: banded FEM block structure plus a few random long-range couplings."""
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    k_band = int(nnz_per_row * 0.8)
+    k_rand = nnz_per_row - k_band
+    for r0 in range(0, n, 4096):
+        r = np.arange(r0, min(n, r0 + 4096))
+        off = rng.integers(-band, band + 1, size=(len(r), k_band))
+        c = np.clip(r[:, None] + off, 0, n - 1)
+        c2 = rng.integers(0, n, size=(len(r), k_rand))
+        cc = np.concatenate([c, c2], axis=1)
+        rr = np.repeat(r, cc.shape[1])
+        rows.append(rr)
+        cols.append(cc.reshape(-1))
+    rows = np.concatenate(rows)
+    cols = np.concatenate(cols)
+    key = np.unique(rows.astype(np.int64) * n + cols)
+    return _csr_from_coo(n, n, key // n, key % n)
+
+
+def block_mask(n, block, density, seed):
+    """DLMC-like 2-D mask: 16x16 (block) structured at the given block density."""
+    rng = np.random.default_rng(seed)
+    nb = n // block
+    mask = rng.random((nb, nb)) < density
+    br, bc = np.nonzero(mask)
+    rr = (br[:, None] * block + np.arange(block)[None, :])
+    cc = (bc[:, None] * block + np.arange(block)[None, :])
+    rows = np.repeat(rr, block, axis=1).reshape(-1)
+    cols = np.tile(cc, (1, block)).reshape(-1)
+    return _csr_from_coo(n, n, rows, cols)
+
+
+def uniform_mask(n, density, seed):
+    rng = np.random.default_rng(seed)
+    total = int(n * n * density)
+    key = np.unique(rng.integers(0, n * n, size=int(total * 1.05)))[:total]
+    return _csr_from_coo(n, n, key // n, key % n)
+
+
+def write_mtx(path, M, N, rowptr, colidx, symmetric_header=False):
+    """Write a Matrix Market coordinate pattern file (1-based) in CSR order."""
+    nnz = int(rowptr[-1])
+    rows = np.repeat(np.arange(M, dtype=np.int64), np.diff(rowptr.astype(np.int64)))
+    with open(path, "w") as f:
+        kind = "symmetric" if symmetric_header else "general"
+        f.write(f"%%MatrixMarket matrix coordinate pattern {kind}\n")
+        f.write(f"{M} {N} {nnz}\n")
+        data = np.stack([rows + 1, colidx.astype(np.int64) + 1], axis=1)
+        np.savetxt(f, data, fmt="%d")
