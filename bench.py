@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py — SDDMM GFLOP/s (2*nnz*K) of the BSMR engine on MI355X, reference headline metric.
+
+Step = one SDDMM pass (the fused dense-tile MFMA + residual launch) over the plan of the C2
+workload of BASELINE.json: nips-like 1,500 x 12,419 pattern (~746k nnz; the real nips.mtx is a
+missing blob of the reference), K = 128, fp32 A/B, alpha = delta = 0.3. Reordering happens once
+before timing and is reported separately (the reference's GFLOP/s excludes it too,
+Logger.hpp:178-180). Inputs are resident in HBM when the timed region starts.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak scaling.
+Rank r owns row block r of an N-times taller pattern (each block the C2 pattern), builds that
+block's plan, and holds its own A rows; B is generated on rank 0 and broadcast once over RCCL
+(xGMI) before timing. There is no collective in the data path; value = all ranks' flops / the
+slowest rank's time.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sddmm-gpu_amd"))
+
+METRIC = "SDDMM GFLOP/s (2·nnz·K) + HBM GB/s %peak, K=128, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--alpha", type=float, default=0.3)
+    ap.add_argument("--delta", type=float, default=0.3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
+    """Oracle host SDDMM (host.cpp:45-76 restated), timed on this box's host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    P = np.empty(len(ci), np.float32)
+    lib = O.lib()
+    Af = np.ascontiguousarray(A, np.float32)
+    Bf = np.ascontiguousarray(B, np.float32)
+    lib.orc_sddmm_cpu(c.h, K, Af, Bf, P, threads)  # warm-up
+    times = []
+    t_end = time.perf_counter() + 20.0
+    while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 50):
+        t0 = time.perf_counter()
+        lib.orc_sddmm_cpu(c.h, K, Af, Bf, P, threads)
+        times.append(time.perf_counter() - t0)
+        if len(times) >= 5 and time.perf_counter() > t_end:
+            break
+    med = statistics.median(times)
+    nerr = O.check_data(P, P_gpu)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(2.0 * len(ci) * K / med / 1e9, 3),
+        "unit": "GFLOP/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full C2 workload (nnz={len(ci)}, K={K}), median of {len(times)} runs "
+                  f"after 1 warm-up, OpenMP over rows; cpu: {model}",
+        "ms": round(med * 1e3, 3),
+        "checkData_errors_vs_gpu": nerr,
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    from bsmr import Plan, make_data, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    K = args.K
+    M, N, rp, ci = synth.nips_like()
+    nnz = len(ci)
+    t0 = time.perf_counter()
+    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, device=dev.index)
+    plan_s = time.perf_counter() - t0
+    st = plan.stats()
+
+    A = make_data(M * K)  # this rank's A rows (Matrix<float>(M,K,row_major).makeData)
+    dA = torch.from_numpy(A).to(dev)
+    if rank == 0:
+        B = make_data(N * K)
+        dB = torch.from_numpy(B).to(dev)
+    else:
+        B = None
+        dB = torch.empty(N * K, dtype=torch.float32, device=dev)
+    bcast_ms = 0.0
+    if dist is not None:
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        dist.broadcast(dB, src=0)  # B broadcast once over RCCL/xGMI
+        torch.cuda.synchronize()
+        bcast_ms = (time.perf_counter() - tb) * 1e3
+    dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    for _ in range(args.warmup):
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ms = e0.elapsed_time(e1)
+    if dist is not None:
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    ms_per_step = ms / args.steps
+
+    # per-part timing of the same kernel (dense-tile items only / residual items only)
+    prof = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=20, stream=sp)
+    P_gpu = dP.cpu().numpy()
+
+    flops_rank = 2.0 * nnz * K
+    value = flops_rank * world / (ms_per_step * 1e-3) / 1e9
+    bytes_alg = 4.0 * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
+    achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "C2: nips_like 1500x12419 (Zipf 1.1 columns, seed 20250801), K=128, "
+                        "fp32 A/B, BSMR alpha=0.3 delta=0.3, 1 plan per rank (row block)",
+            "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
+            "parallelism": f"row-panel blocks x{world}, B broadcast (RCCL)",
+            "num_clusters": st["num_clusters"], "dense_tiles": st["num_dense_tiles"],
+            "residual_nnz": st["num_residual"], "dense_items": st["dense_items"],
+            "residual_items": st["residual_items"],
+            "plan_build_s": round(plan_s, 3), "row_reorder_ms": round(st["row_reorder_ms"], 3),
+            "col_reorder_ms": round(st["col_reorder_ms"], 3), "b_broadcast_ms": round(bcast_ms, 3),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "k_sddmm_f32<128,16> (fused dense MFMA + residual)",
+            "bytes_alg_per_launch": bytes_alg,
+        },
+        "kernels_ms": {k: round(v, 5) for k, v in prof.items()},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(M, N, rp, ci, K, A, B, P_gpu)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * bsmr.h — C ABI of the MI355X-native BSMR-SDDMM engine (libbsmr_amd.so).
+ *
+ * Drop-in boundary for the reference BSMR-SDDMM hot path (CX9898/sddmm-gpu): plain pointers and
+ * sizes, int status codes, no exceptions, plan-owned device memory, caller-owned streams.
+ * Each entry point names the reference interface it replaces (paths relative to the reference
+ * repository root). Reference-side bindings a maintainer would add: INTEGRATION.md.
+ *
+ * Layouts (same as the reference):
+ *   S : CSR, rowptr[M+1] and colidx[nnz] (uint32), column order inside a row = file order.
+ *   A : M x K row-major            A[r*K + k]        (Matrix<float>(M,K,row_major), main.cu:23)
+ *   B : K x N column-major         B[c*K + k]        (Matrix<float>(K,N,col_major), main.cu:26)
+ *   P : nnz values in CSR order    P[idx] = sum_k A[row(idx)*K+k] * B[col(idx)*K+k]
+ */
+#ifndef BSMR_AMD_H
+#define BSMR_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSMR_ABI_VERSION 1
+
+typedef enum {
+    BSMR_OK = 0,
+    BSMR_ERR_INVALID = 1,     /* bad argument / shape */
+    BSMR_ERR_IO = 2,          /* file cannot be opened or parsed */
+    BSMR_ERR_REJECTED = 3,    /* matrix rejected by the reference loader rules */
+    BSMR_ERR_HIP = 4,         /* HIP runtime error (message via bsmr_last_error) */
+    BSMR_ERR_TIMEOUT = 5,     /* a persistent reorder kernel gave up waiting (never expected) */
+    BSMR_ERR_UNSUPPORTED = 6  /* e.g. K not a multiple of 16, dtype not built */
+} bsmr_status;
+
+typedef enum { BSMR_F32 = 0, BSMR_F16 = 1, BSMR_BF16 = 2 } bsmr_dtype;
+
+/* Last error message of the calling thread ("" if none). */
+const char* bsmr_last_error(void);
+int bsmr_abi_version(void);
+
+/* ------------------------------------------------------------------ host matrix input ---- */
+typedef struct bsmr_csr bsmr_csr;
+
+/* Replaces sparseMatrix::CSR<float>::initializeFromMatrixFile / initializeFromMtxFile
+ * (src/Matrix.cpp:279-294, 398-480). Same acceptance/rejection rules and messages; verbose != 0
+ * prints "sparseMatrix::CSR initialize from file : <f>" like the reference. */
+int bsmr_csr_load_mtx(const char* path, int verbose, bsmr_csr** out);
+/* Wrap caller arrays (copied). */
+int bsmr_csr_create(uint32_t M, uint32_t N, uint32_t nnz, const uint32_t* rowptr,
+                    const uint32_t* colidx, bsmr_csr** out);
+void bsmr_csr_info(const bsmr_csr* s, uint32_t* M, uint32_t* N, uint32_t* nnz);
+const uint32_t* bsmr_csr_rowptr(const bsmr_csr* s);
+const uint32_t* bsmr_csr_colidx(const bsmr_csr* s);
+const float* bsmr_csr_values(const bsmr_csr* s);
+void bsmr_csr_free(bsmr_csr* s);
+
+/* Replaces Matrix<T>::makeData (src/Matrix.cpp:117-138): n values of a fresh default-seeded
+ * std::mt19937 through uniform_real_distribution<float>(0,2), generated single-threaded
+ * (the reference's OpenMP loop shares one engine across threads). */
+void bsmr_make_data(uint64_t n, float* out);
+
+/* ------------------------------------------------------------------------ the plan ---- */
+typedef struct bsmr_plan bsmr_plan;
+
+typedef struct {
+    float alpha;              /* similarity threshold  (Options -a, default 0.3) */
+    float delta;              /* tile density threshold (Options -d, default 0.3) */
+    uint64_t free_mem_bytes;  /* calculateBlockSize input; 0 = query the device (hipMemGetInfo) */
+    int device;               /* HIP device ordinal */
+    uint32_t cluster_batch;   /* clusters per persistent launch; 0 = default */
+    int exact_similarity;     /* !=0: evaluate every similarity with the exact fp32 tree */
+} bsmr_plan_options;
+
+void bsmr_plan_options_default(bsmr_plan_options* o);
+
+/* Replaces BSMR::BSMR(alpha, delta, S) + RPHM::RPHM(S, bsmr) (src/BSMR.cpp:16-265;
+ * include/BSMR.hpp:25-28, 83-159): row reordering (rowReordering.cu:1027-1095), column
+ * reordering (colReordering.cu:274-404) and the dense-tile / residual layout, all built on the
+ * GPU. Host CSR in, device-resident plan out. */
+int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M, uint32_t N,
+                     uint32_t nnz, const bsmr_plan_options* opt, bsmr_plan** out);
+/* Test-mode split (sddmm.cu:62-118): keep the row reordering, redo the column split for delta. */
+int bsmr_plan_recolumn(bsmr_plan* plan, float delta);
+void bsmr_plan_destroy(bsmr_plan* plan);
+
+typedef struct {
+    uint32_t M, N, nnz;
+    uint32_t block_size;             /* calculateBlockSize */
+    uint32_t num_blocks_per_row;     /* nbpr */
+    uint32_t cluster_block_dim;      /* B(nbpr) of bsa_clustering */
+    int32_t num_clusters;            /* bsmr_numClusters (incl. the reference quirk) */
+    uint32_t num_row_panels;         /* NumRowPanel */
+    uint32_t num_reordered_rows;
+    uint32_t num_dense_tiles;        /* blockOffsets.back() */
+    uint32_t max_dense_tiles_per_panel;
+    uint32_t num_residual;           /* sparseValueOffsets.back() */
+    uint32_t num_dense_thread_blocks;   /* reference launch shape numbers, for the log */
+    uint32_t num_sparse_thread_blocks;
+    uint64_t exact_similarity_evals;
+    uint64_t total_similarity_evals;
+    float row_reorder_ms;            /* bsmr_rowReordering */
+    float col_reorder_ms;            /* bsmr_colReordering (incl. tile layout) */
+    uint32_t dense_items, residual_items;  /* work-list sizes of the SDDMM launch */
+} bsmr_plan_stats;
+
+int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);
+
+/* Parity dumps: copy one plan array to host. *len receives the element count; host_out may be
+ * NULL to query the length. Arrays are the reference RPHM/BSMR members. */
+typedef enum {
+    BSMR_ARR_REORDERED_ROWS = 0,
+    BSMR_ARR_DENSE_COLS = 1,
+    BSMR_ARR_DENSE_COL_OFFSETS = 2,
+    BSMR_ARR_SPARSE_COLS = 3,
+    BSMR_ARR_SPARSE_COL_OFFSETS = 4,
+    BSMR_ARR_SPARSE_VALUE_OFFSETS = 5,
+    BSMR_ARR_BLOCK_OFFSETS = 6,
+    BSMR_ARR_BLOCK_VALUES = 7,
+    BSMR_ARR_SPARSE_VALUES = 8,
+    BSMR_ARR_SPARSE_RELATIVE_ROWS = 9,
+    BSMR_ARR_SPARSE_COL_INDICES = 10,
+    BSMR_ARR_DISPERSION = 11,      /* per original row */
+    BSMR_ARR_ASCENDING = 12        /* rows stably sorted by dispersion */
+} bsmr_array;
+int bsmr_plan_get_array(const bsmr_plan* plan, int which, uint32_t* host_out, uint64_t* len);
+
+/* Reorder-quality statistics printed by the reference log (evaluationReordering,
+ * BSMR.cpp:826-994), evaluated on the host from the plan arrays (log only, not timed). */
+typedef struct {
+    int32_t num_dense_block;          /* bsmr_numDenseBlock */
+    float average_density;            /* bsmr_averageDensity */
+    int32_t original_num_dense_block; /* original_numDenseBlock */
+    float original_average_density;   /* original_averageDensity */
+    int32_t num_dense_data;           /* bsmr_numDenseData */
+    int32_t num_sparse_data;          /* bsmr_numSparseData */
+} bsmr_eval_stats;
+int bsmr_plan_evaluate(const bsmr_plan* plan, bsmr_eval_stats* out);
+
+/* ------------------------------------------------------------------------- SDDMM ---- */
+/* Replaces sddmm_gpu(M, N, K, dA, dB, rphm, dP, logger) (include/sddmmKernel.cuh:25-30,
+ * src/sddmmKernel.cu:2540-2762): device pointers, dA row-major M x K, dB column-major K x N,
+ * dP (fp32, nnz, CSR order) overwritten. dtype selects the A/B element type (fp32, or fp16/bf16
+ * with fp32 accumulation). stream: a hipStream_t (NULL = default stream). Asynchronous. */
+int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K, int dtype,
+               float* dP, void* stream);
+
+/* Row-panel sharding for multi-GPU runs: contiguous panel ranges balanced by a
+ * cost model; bsmr_sddmm_panels computes only the outputs of panels [p0, p1). */
+int bsmr_plan_shard(const bsmr_plan* plan, uint32_t K, int rank, int world, uint32_t* p0,
+                    uint32_t* p1);
+/* The same cost model on host offset arrays (no device): cuts[world+1], cuts[0]=0, cuts[world]=P. */
+int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* sparseValueOffsets, uint32_t P,
+                    uint32_t K, int world, uint32_t* cuts);
+int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
+                      int dtype, float* dP, uint32_t p0, uint32_t p1, void* stream);
+
+/* Timing: run `iters` back-to-back SDDMMs on `stream`, timing each kernel with HIP events on
+ * that stream. Outputs average ms per launch of the dense-tile kernel, the residual kernel and
+ * the whole SDDMM. */
+int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
+                       int dtype, float* dP, int iters, void* stream, float* ms_dense,
+                       float* ms_residual, float* ms_total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSMR_AMD_H */

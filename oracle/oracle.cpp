@@ -102,8 +102,8 @@ int three_words(const std::string& line, u32& a, u32& b, T& c) {
     char* endp = nullptr;
     const double d = std::strtod(w.c_str(), &endp);
     if (endp == w.c_str()) return -1;  // stod invalid_argument
-    if (errno == ERANGE && (d == HUGE_VAL || d == -HUGE_VAL || d == 0.0)) {
-        // std::stod reports out_of_range for overflow and for underflow (glibc sets ERANGE)
+    if (errno == ERANGE) {
+        // libstdc++ std::stod throws out_of_range whenever strtod sets ERANGE
         std::cout << "Warning: valueStr out of range: " << w << std::endl;
         c = static_cast<T>(0);
         return 1;

@@ -1,0 +1,266 @@
+"""Python host mirror of the reference BSMR-SDDMM interface, over libbsmr_amd.so (include/bsmr.h).
+
+Reference interface mirrored (paths relative to the reference root):
+  * sparseMatrix::CSR<float>::initializeFromMatrixFile -> load_mtx        (src/Matrix.cpp:279-480)
+  * Matrix<float>::makeData                            -> make_data       (src/Matrix.cpp:117-138)
+  * BSMR(alpha, delta, S) + RPHM(S, bsmr)              -> Plan            (src/BSMR.cpp:16-265)
+  * sddmm_gpu(M, N, K, dA, dB, rphm, dP, logger)       -> Plan.sddmm      (src/sddmmKernel.cu:2540)
+  * evaluationReordering                               -> Plan.evaluate   (src/BSMR.cpp:826-994)
+
+Every call goes through the HIP library; there is no CPU fallback. If the shared library is
+missing the import fails loudly (build it with `make -C sddmm-gpu_amd` or
+`python -c "import __graft_entry__ as g; g.build()"`).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libbsmr_amd.so")
+
+F32, F16, BF16 = 0, 1, 2
+
+ARRAYS = {
+    "reorderedRows": 0, "denseCols": 1, "denseColOffsets": 2, "sparseCols": 3,
+    "sparseColOffsets": 4, "sparseValueOffsets": 5, "blockOffsets": 6, "blockValues": 7,
+    "sparseValues": 8, "sparseRelativeRows": 9, "sparseColIndices": 10, "dispersion": 11,
+    "ascending": 12,
+}
+
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+
+
+class BsmrError(RuntimeError):
+    pass
+
+
+class PlanOptions(C.Structure):
+    _fields_ = [("alpha", C.c_float), ("delta", C.c_float), ("free_mem_bytes", C.c_uint64),
+                ("device", C.c_int), ("cluster_batch", C.c_uint32),
+                ("exact_similarity", C.c_int)]
+
+
+class PlanStats(C.Structure):
+    _fields_ = [("M", C.c_uint32), ("N", C.c_uint32), ("nnz", C.c_uint32),
+                ("block_size", C.c_uint32), ("num_blocks_per_row", C.c_uint32),
+                ("cluster_block_dim", C.c_uint32), ("num_clusters", C.c_int32),
+                ("num_row_panels", C.c_uint32), ("num_reordered_rows", C.c_uint32),
+                ("num_dense_tiles", C.c_uint32), ("max_dense_tiles_per_panel", C.c_uint32),
+                ("num_residual", C.c_uint32), ("num_dense_thread_blocks", C.c_uint32),
+                ("num_sparse_thread_blocks", C.c_uint32),
+                ("exact_similarity_evals", C.c_uint64), ("total_similarity_evals", C.c_uint64),
+                ("row_reorder_ms", C.c_float), ("col_reorder_ms", C.c_float),
+                ("dense_items", C.c_uint32), ("residual_items", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class EvalStats(C.Structure):
+    _fields_ = [("num_dense_block", C.c_int32), ("average_density", C.c_float),
+                ("original_num_dense_block", C.c_int32), ("original_average_density", C.c_float),
+                ("num_dense_data", C.c_int32), ("num_sparse_data", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every symbol include/bsmr.h declares (tests check the library exports all of them)
+EXPORTS = [
+    "bsmr_last_error", "bsmr_abi_version", "bsmr_csr_load_mtx", "bsmr_csr_create",
+    "bsmr_csr_info", "bsmr_csr_rowptr", "bsmr_csr_colidx", "bsmr_csr_values", "bsmr_csr_free",
+    "bsmr_make_data", "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
+    "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
+    "bsmr_sddmm", "bsmr_plan_shard", "bsmr_shard_cuts", "bsmr_sddmm_panels",
+    "bsmr_sddmm_profile",
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BsmrError(f"HIP extension not built: {LIB_PATH} is missing "
+                        "(run `make -C sddmm-gpu_amd`)")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.bsmr_last_error.restype = C.c_char_p
+    L.bsmr_abi_version.restype = C.c_int
+    L.bsmr_csr_load_mtx.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+    L.bsmr_csr_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p, C.POINTER(vp)]
+    L.bsmr_csr_info.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                C.POINTER(C.c_uint32)]
+    L.bsmr_csr_rowptr.restype = C.POINTER(C.c_uint32)
+    L.bsmr_csr_rowptr.argtypes = [vp]
+    L.bsmr_csr_colidx.restype = C.POINTER(C.c_uint32)
+    L.bsmr_csr_colidx.argtypes = [vp]
+    L.bsmr_csr_values.restype = C.POINTER(C.c_float)
+    L.bsmr_csr_values.argtypes = [vp]
+    L.bsmr_csr_free.argtypes = [vp]
+    L.bsmr_make_data.argtypes = [C.c_uint64, _f32p]
+    L.bsmr_plan_options_default.argtypes = [C.POINTER(PlanOptions)]
+    L.bsmr_plan_create.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.POINTER(PlanOptions), C.POINTER(vp)]
+    L.bsmr_plan_recolumn.argtypes = [vp, C.c_float]
+    L.bsmr_plan_destroy.argtypes = [vp]
+    L.bsmr_plan_get_stats.argtypes = [vp, C.POINTER(PlanStats)]
+    L.bsmr_plan_get_array.argtypes = [vp, C.c_int, vp, C.POINTER(C.c_uint64)]
+    L.bsmr_plan_evaluate.argtypes = [vp, C.POINTER(EvalStats)]
+    L.bsmr_sddmm.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, vp]
+    L.bsmr_plan_shard.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32),
+                                  C.POINTER(C.c_uint32)]
+    L.bsmr_shard_cuts.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_int, _u32p]
+    L.bsmr_sddmm_panels.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
+                                    C.c_uint32, vp]
+    L.bsmr_sddmm_profile.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_int, vp,
+                                     C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                     C.POINTER(C.c_float)]
+    _lib = L
+    return L
+
+
+def _check(status, what):
+    if status != 0:
+        msg = lib().bsmr_last_error().decode(errors="replace")
+        raise BsmrError(f"{what} failed with status {status}: {msg}")
+
+
+def make_data(n):
+    """Matrix<float>::makeData stream: default-seeded mt19937, uniform [0, 2)."""
+    out = np.empty(int(n), np.float32)
+    lib().bsmr_make_data(out.size, out)
+    return out
+
+
+class Csr:
+    """Host CSR (uint32 rowptr/colidx), as sparseMatrix::CSR<float>."""
+
+    def __init__(self, handle):
+        self.h = handle
+        M, N, nnz = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        lib().bsmr_csr_info(handle, C.byref(M), C.byref(N), C.byref(nnz))
+        self.M, self.N, self.nnz = M.value, N.value, nnz.value
+
+    @classmethod
+    def load_mtx(cls, path, verbose=False):
+        h = C.c_void_p()
+        st = lib().bsmr_csr_load_mtx(path.encode(), 1 if verbose else 0, C.byref(h))
+        if st != 0:
+            return None
+        return cls(h)
+
+    @classmethod
+    def from_arrays(cls, M, N, rowptr, colidx):
+        rowptr = np.ascontiguousarray(rowptr, np.uint32)
+        colidx = np.ascontiguousarray(colidx, np.uint32)
+        h = C.c_void_p()
+        _check(lib().bsmr_csr_create(M, N, len(colidx), rowptr, colidx, C.byref(h)),
+               "bsmr_csr_create")
+        return cls(h)
+
+    @property
+    def rowptr(self):
+        return np.ctypeslib.as_array(lib().bsmr_csr_rowptr(self.h), shape=(self.M + 1,)).copy()
+
+    @property
+    def colidx(self):
+        return np.ctypeslib.as_array(lib().bsmr_csr_colidx(self.h), shape=(self.nnz,)).copy()
+
+    @property
+    def values(self):
+        return np.ctypeslib.as_array(lib().bsmr_csr_values(self.h), shape=(self.nnz,)).copy()
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.bsmr_csr_free(self.h)
+            self.h = None
+
+
+def load_mtx(path, verbose=False):
+    return Csr.load_mtx(path, verbose)
+
+
+class Plan:
+    """Device-resident BSMR plan (reordered rows, dense 16x16 tiles, residual lists)."""
+
+    def __init__(self, M, N, rowptr, colidx, alpha=0.3, delta=0.3, free_mem_bytes=0, device=0,
+                 cluster_batch=0, exact_similarity=False):
+        rowptr = np.ascontiguousarray(rowptr, np.uint32)
+        colidx = np.ascontiguousarray(colidx, np.uint32)
+        o = PlanOptions()
+        lib().bsmr_plan_options_default(C.byref(o))
+        o.alpha = float(np.float32(alpha))
+        o.delta = float(np.float32(delta))
+        o.free_mem_bytes = int(free_mem_bytes)
+        o.device = int(device)
+        o.cluster_batch = int(cluster_batch)
+        o.exact_similarity = 1 if exact_similarity else 0
+        self.M, self.N, self.nnz = int(M), int(N), int(len(colidx))
+        h = C.c_void_p()
+        _check(lib().bsmr_plan_create(rowptr, colidx, M, N, len(colidx), C.byref(o), C.byref(h)),
+               "bsmr_plan_create")
+        self.h = h
+
+    def recolumn(self, delta):
+        _check(lib().bsmr_plan_recolumn(self.h, float(np.float32(delta))), "bsmr_plan_recolumn")
+
+    def stats(self):
+        s = PlanStats()
+        _check(lib().bsmr_plan_get_stats(self.h, C.byref(s)), "bsmr_plan_get_stats")
+        return s.as_dict()
+
+    def array(self, name):
+        which = ARRAYS[name]
+        n = C.c_uint64()
+        _check(lib().bsmr_plan_get_array(self.h, which, None, C.byref(n)), "bsmr_plan_get_array")
+        out = np.empty(n.value, np.uint32)
+        if n.value:
+            _check(lib().bsmr_plan_get_array(self.h, which, out.ctypes.data, C.byref(n)),
+                   "bsmr_plan_get_array")
+        return out
+
+    def evaluate(self):
+        e = EvalStats()
+        _check(lib().bsmr_plan_evaluate(self.h, C.byref(e)), "bsmr_plan_evaluate")
+        return e.as_dict()
+
+    def sddmm(self, dA, dB, K, dP, stream=0, dtype=F32):
+        """dA, dB, dP: device pointers (int) — e.g. torch tensor .data_ptr()."""
+        _check(lib().bsmr_sddmm(self.h, dA, dB, K, dtype, dP, stream or None), "bsmr_sddmm")
+
+    def sddmm_panels(self, dA, dB, K, dP, p0, p1, stream=0, dtype=F32):
+        _check(lib().bsmr_sddmm_panels(self.h, dA, dB, K, dtype, dP, p0, p1, stream or None),
+               "bsmr_sddmm_panels")
+
+    def shard(self, K, rank, world):
+        p0, p1 = C.c_uint32(), C.c_uint32()
+        _check(lib().bsmr_plan_shard(self.h, K, rank, world, C.byref(p0), C.byref(p1)),
+               "bsmr_plan_shard")
+        return p0.value, p1.value
+
+    def profile(self, dA, dB, K, dP, iters=10, stream=0, dtype=F32):
+        d, r, t = C.c_float(), C.c_float(), C.c_float()
+        _check(lib().bsmr_sddmm_profile(self.h, dA, dB, K, dtype, dP, iters, stream or None,
+                                        C.byref(d), C.byref(r), C.byref(t)),
+               "bsmr_sddmm_profile")
+        return {"dense_ms": d.value, "residual_ms": r.value, "total_ms": t.value}
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.bsmr_plan_destroy(self.h)
+            self.h = None
+
+
+def shard_cuts(block_offsets, sparse_value_offsets, K, world):
+    """Panel cut points [0 = c_0 <= ... <= c_world = P] of the row-panel sharding cost model."""
+    bo = np.ascontiguousarray(block_offsets, np.uint32)
+    so = np.ascontiguousarray(sparse_value_offsets, np.uint32)
+    P = len(bo) - 1
+    cuts = np.zeros(world + 1, np.uint32)
+    _check(lib().bsmr_shard_cuts(bo, so, P, K, world, cuts), "bsmr_shard_cuts")
+    return cuts

@@ -1,0 +1,264 @@
+// capi.cpp — plan lifecycle, parity dumps, reorder statistics and sharding of the C ABI.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+#include "plan.hpp"
+
+using namespace bsmr;
+
+extern "C" void bsmr_plan_options_default(bsmr_plan_options* o) {
+    o->alpha = 0.3f;   // Options.hpp:40
+    o->delta = 0.3f;   // Options.hpp:41
+    o->free_mem_bytes = 0;
+    o->device = 0;
+    o->cluster_batch = 0;
+    o->exact_similarity = 0;
+}
+
+extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M,
+                                uint32_t N, uint32_t nnz, const bsmr_plan_options* opt,
+                                bsmr_plan** out) {
+    *out = nullptr;
+    if (!rowptr || !colidx || M == 0 || N == 0 || rowptr[M] != nnz || nnz < 2) {
+        set_error("bsmr_plan_create: invalid CSR (need rowptr[M] == nnz >= 2)");
+        return BSMR_ERR_INVALID;
+    }
+    bsmr_plan_options o;
+    if (opt)
+        o = *opt;
+    else
+        bsmr_plan_options_default(&o);
+    auto* h = new bsmr_plan;
+    Plan& p = h->p;
+    auto fail = [&](int st) {
+        delete h;
+        return st;
+    };
+    p.device = o.device;
+    if (hipSetDevice(o.device) != hipSuccess) {
+        set_error("bsmr_plan_create: hipSetDevice failed");
+        return fail(BSMR_ERR_HIP);
+    }
+    if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("bsmr_plan_create: hipStreamCreate failed");
+        return fail(BSMR_ERR_HIP);
+    }
+    p.M = M;
+    p.N = N;
+    p.nnz = nnz;
+    p.alpha = o.alpha;
+    p.delta = o.delta;
+    p.exact_all = o.exact_similarity;
+    if (o.cluster_batch) p.cluster_batch = o.cluster_batch;
+    u64 free_mem = o.free_mem_bytes;
+    if (free_mem == 0) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+            set_error("bsmr_plan_create: hipMemGetInfo failed");
+            return fail(BSMR_ERR_HIP);
+        }
+        free_mem = fr;
+    }
+    p.bs = block_size_for(M, N, free_mem);
+    if (p.bs > 65535) {
+        set_error("bsmr_plan_create: column block size exceeds 16-bit encoding");
+        return fail(BSMR_ERR_UNSUPPORTED);
+    }
+    p.nbpr = static_cast<u32>(std::ceil(static_cast<float>(N) / static_cast<float>(p.bs)));  // rowReordering.cu:1035
+    p.B = cluster_block_dim(p.nbpr);
+    p.keptMask = kept_warp_mask(p.B);
+    int st = p.build_rows(rowptr, colidx);
+    if (st != BSMR_OK) return fail(st);
+    st = p.build_columns();
+    if (st != BSMR_OK) return fail(st);
+    *out = h;
+    return BSMR_OK;
+}
+
+extern "C" int bsmr_plan_recolumn(bsmr_plan* plan, float delta) {
+    if (!plan) return BSMR_ERR_INVALID;
+    plan->p.delta = delta;
+    return plan->p.build_columns();
+}
+
+extern "C" void bsmr_plan_destroy(bsmr_plan* plan) { delete plan; }
+
+extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
+    if (!plan || !s) return BSMR_ERR_INVALID;
+    const Plan& p = plan->p;
+    std::memset(s, 0, sizeof(*s));
+    s->M = p.M;
+    s->N = p.N;
+    s->nnz = p.nnz;
+    s->block_size = p.bs;
+    s->num_blocks_per_row = p.nbpr;
+    s->cluster_block_dim = p.B;
+    s->num_clusters = p.numClusters;
+    s->num_row_panels = p.P;
+    s->num_reordered_rows = p.R;
+    s->num_dense_tiles = p.numDenseTiles;
+    s->max_dense_tiles_per_panel = p.maxTilesPerPanel;
+    s->num_residual = p.nres;
+    s->num_dense_thread_blocks = p.numDenseTB;
+    s->num_sparse_thread_blocks = p.numSparseTB;
+    s->exact_similarity_evals = p.exact_evals;
+    s->total_similarity_evals = p.total_evals;
+    s->row_reorder_ms = p.row_ms;
+    s->col_reorder_ms = p.col_ms;
+    s->dense_items = p.nDenseItems;
+    s->residual_items = p.nResItems;
+    return BSMR_OK;
+}
+
+extern "C" int bsmr_plan_get_array(const bsmr_plan* plan, int which, uint32_t* host_out,
+                                   uint64_t* len) {
+    if (!plan) return BSMR_ERR_INVALID;
+    const Plan& p = plan->p;
+    const DevBuf<u32>* b = nullptr;
+    size_t n = 0;
+    switch (which) {
+        case BSMR_ARR_REORDERED_ROWS: b = &p.rows; n = p.R; break;
+        case BSMR_ARR_DENSE_COLS: b = &p.denseCols; n = p.denseCols.n; break;
+        case BSMR_ARR_DENSE_COL_OFFSETS: b = &p.denseColOffsets; n = p.P + 1; break;
+        case BSMR_ARR_SPARSE_COLS: b = &p.sparseCols; n = p.sparseCols.n; break;
+        case BSMR_ARR_SPARSE_COL_OFFSETS: b = &p.sparseColOffsets; n = p.P + 1; break;
+        case BSMR_ARR_SPARSE_VALUE_OFFSETS: b = &p.sparseValueOffsets; n = p.P + 1; break;
+        case BSMR_ARR_BLOCK_OFFSETS: b = &p.blockOffsets; n = p.P + 1; break;
+        case BSMR_ARR_BLOCK_VALUES: b = &p.blockValues; n = p.blockValues.n; break;
+        case BSMR_ARR_SPARSE_VALUES: b = &p.sparseValues; n = p.nres; break;
+        case BSMR_ARR_SPARSE_RELATIVE_ROWS: b = &p.sparseRel; n = p.nres; break;
+        case BSMR_ARR_SPARSE_COL_INDICES: b = &p.sparseColIdx; n = p.nres; break;
+        case BSMR_ARR_DISPERSION: b = &p.disp; n = p.M; break;
+        case BSMR_ARR_ASCENDING: b = &p.asc; n = p.M; break;
+        default:
+            set_error("bsmr_plan_get_array: unknown array");
+            return BSMR_ERR_INVALID;
+    }
+    if (len) *len = n;
+    if (host_out && n) {
+        BSMR_HIP(hipSetDevice(p.device));
+        BSMR_HIP(hipMemcpy(host_out, b->data(), n * sizeof(u32), hipMemcpyDeviceToHost));
+    }
+    return BSMR_OK;
+}
+
+// evaluationReordering + calculateNumDenseBlocksAndAverageDensityInOriginalMatrix
+// (BSMR.cpp:826-930, 955-994), evaluated on the host from the plan arrays (log statistics only;
+// not on the timed path). Float accumulation order follows the reference loops.
+extern "C" int bsmr_plan_evaluate(const bsmr_plan* plan, bsmr_eval_stats* out) {
+    if (!plan || !out) return BSMR_ERR_INVALID;
+    const Plan& p = plan->p;
+    BSMR_HIP(hipSetDevice(p.device));
+    std::vector<u32> rowptr, col, rows, dco, dcols, sco, scols;
+    BSMR_CHECK(p.rowptr.download(rowptr, p.stream));
+    BSMR_CHECK(p.colidx.download(col, p.stream));
+    BSMR_CHECK(p.rows.download(rows, p.stream));
+    BSMR_CHECK(p.denseColOffsets.download(dco, p.stream));
+    BSMR_CHECK(p.denseCols.download(dcols, p.stream));
+    BSMR_CHECK(p.sparseColOffsets.download(sco, p.stream));
+    BSMR_CHECK(p.sparseCols.download(scols, p.stream));
+    rows.resize(p.R);
+    const u32 N = p.N;
+    int numDense = 0, numSparseData = 0;
+    float total = 0.f;
+    std::vector<u32> blockOf(N + 1, NULLV);
+    std::vector<char> isSparse(N + 1, 0);
+    for (u32 q = 0; q < p.P; ++q) {
+        const u32 d0 = dco[q], d1 = dco[q + 1], s0 = sco[q], s1 = sco[q + 1];
+        const u32 nDB = (d1 - d0 + 15) / 16;
+        for (u32 j = d0; j < d1; ++j) blockOf[dcols[j]] = (j - d0) / 16;
+        for (u32 j = s0; j < s1; ++j) isSparse[scols[j]] = 1;
+        std::vector<u32> cnt(nDB, 0);
+        const u32 r1 = std::min(q * 16 + 16, p.R);
+        for (u32 x = q * 16; x < r1; ++x)
+            for (u32 k = rowptr[rows[x]]; k < rowptr[rows[x] + 1]; ++k) {
+                if (blockOf[col[k]] != NULLV) ++cnt[blockOf[col[k]]];
+                if (isSparse[col[k]]) ++numSparseData;
+            }
+        for (u32 b = 0; b < nDB; ++b)
+            if (cnt[b] > 0) {
+                const float density = static_cast<float>(cnt[b]) / 256.0f;
+                total += density;
+                if (density >= p.delta) ++numDense;
+            }
+        for (u32 j = d0; j < d1; ++j) blockOf[dcols[j]] = NULLV;
+        for (u32 j = s0; j < s1; ++j) isSparse[scols[j]] = 0;
+    }
+    out->num_dense_block = numDense;
+    const float avg = total / static_cast<float>(numDense);
+    out->average_density = avg > 0 ? avg : 0.0f;
+    out->num_sparse_data = numSparseData;
+    out->num_dense_data = static_cast<int32_t>(p.nnz) - numSparseData;
+    // original-order tiles
+    const u32 OP = (p.M + 15) / 16;
+    u32 onum = 0;
+    float ototal = 0.f;
+    std::vector<u32> cb;
+    for (u32 q = 0; q < OP; ++q) {
+        cb.clear();
+        const u32 r0 = q * 16, r1 = std::min(r0 + 16, p.M);
+        for (u32 r = r0; r < r1; ++r)
+            for (u32 k = rowptr[r]; k < rowptr[r + 1]; ++k) cb.push_back(col[k] / 16);
+        std::sort(cb.begin(), cb.end());
+        for (size_t k = 0; k < cb.size();) {
+            size_t j = k;
+            while (j < cb.size() && cb[j] == cb[k]) ++j;
+            const u32 c0 = cb[k] * 16, c1 = std::min(c0 + 16, N);
+            const float bsz = static_cast<float>((r1 - r0) * (c1 - c0));
+            const float density = static_cast<float>(j - k) / bsz;
+            if (density >= p.delta) {
+                ototal += density;
+                ++onum;
+            }
+            k = j;
+        }
+    }
+    out->original_num_dense_block = static_cast<int32_t>(onum);
+    out->original_average_density = onum > 0 ? ototal / static_cast<float>(onum) : 0.0f;
+    return BSMR_OK;
+}
+
+// Contiguous panel ranges balanced by a cost model: a dense tile costs 256*K MACs on the matrix
+// core, priced at 1/4 of a residual MAC (fp32 MFMA vs. gathered scalar FMA); a residual entry
+// costs K; every panel costs 1 (its A rows). cuts[0] = 0, cuts[world] = P, non-decreasing.
+extern "C" int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* sparseValueOffsets,
+                               uint32_t P, uint32_t K, int world, uint32_t* cuts) {
+    if (!blockOffsets || !sparseValueOffsets || !cuts || world <= 0) {
+        set_error("bsmr_shard_cuts: bad arguments");
+        return BSMR_ERR_INVALID;
+    }
+    std::vector<double> cum(P + 1ull, 0.0);
+    for (u32 q = 0; q < P; ++q) {
+        const double tiles = blockOffsets[q + 1] - blockOffsets[q];
+        const double res = sparseValueOffsets[q + 1] - sparseValueOffsets[q];
+        cum[q + 1] = cum[q] + tiles * 64.0 * K + res * K + 1.0;
+    }
+    cuts[0] = 0;
+    for (int r = 1; r < world; ++r) {
+        const double target = cum[P] * r / world;
+        u32 c = static_cast<u32>(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        c = std::min(std::max(c, cuts[r - 1]), P);
+        cuts[r] = c;
+    }
+    cuts[world] = P;
+    return BSMR_OK;
+}
+
+extern "C" int bsmr_plan_shard(const bsmr_plan* plan, uint32_t K, int rank, int world,
+                               uint32_t* p0, uint32_t* p1) {
+    if (!plan || world <= 0 || rank < 0 || rank >= world) {
+        set_error("bsmr_plan_shard: bad arguments");
+        return BSMR_ERR_INVALID;
+    }
+    const Plan& p = plan->p;
+    std::vector<u32> cuts(world + 1);
+    BSMR_CHECK(bsmr_shard_cuts(p.h_blockOffsets.data(), p.h_sparseValueOffsets.data(), p.P, K,
+                               world, cuts.data()));
+    *p0 = cuts[rank];
+    *p1 = cuts[rank + 1];
+    return BSMR_OK;
+}

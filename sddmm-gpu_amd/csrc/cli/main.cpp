@@ -1,0 +1,199 @@
+// main.cpp — BSMR-sddmm: drop-in for the reference binary (src/main.cu:6-42, src/sddmm.cu:10-118).
+// A thin client of libbsmr_amd.so: load S, generate A (M x K row-major) and B (K x N col-major)
+// with makeData, build the BSMR plan on the GPU, run 10 timed SDDMM iterations, print the log.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "bsmr.h"
+#include "logger.hpp"
+#include "options.hpp"
+
+namespace {
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::cerr << "HIP error: " << hipGetErrorString(e_) << " at " << #x << std::endl; \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+void die(const char* what, int st) {
+    std::cerr << what << " failed (" << st << "): " << bsmr_last_error() << std::endl;
+    std::exit(1);
+}
+
+struct Dev {
+    void* p = nullptr;
+    explicit Dev(size_t bytes) { HIPCHK(hipMalloc(&p, bytes ? bytes : 4)); }
+    ~Dev() { (void)hipFree(p); }
+};
+
+// one reference "sddmm(options, A, B, P, logger)" run on an existing plan (sddmm.cu:10-39)
+void run_sddmm(bsmr_plan* plan, const bsmr_csr* S, uint32_t K, int iters, cli::Logger& log,
+               std::vector<float>* P_out) {
+    uint32_t M, N, nnz;
+    bsmr_csr_info(S, &M, &N, &nnz);
+    std::vector<float> A(static_cast<size_t>(M) * K), B(static_cast<size_t>(N) * K);
+    bsmr_make_data(A.size(), A.data());  // Matrix<float>(M,K,row_major).makeData()
+    bsmr_make_data(B.size(), B.data());  // Matrix<float>(K,N,col_major).makeData()
+    Dev dA(A.size() * 4), dB(B.size() * 4), dP(static_cast<size_t>(nnz) * 4);
+    HIPCHK(hipMemcpy(dA.p, A.data(), A.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dB.p, B.data(), B.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(dP.p, 0, static_cast<size_t>(nnz) * 4));
+    hipStream_t s;
+    HIPCHK(hipStreamCreate(&s));
+    float* P = static_cast<float*>(dP.p);
+    int st = bsmr_sddmm(plan, dA.p, dB.p, K, BSMR_F32, P, s);  // warm-up (code object load)
+    if (st) die("bsmr_sddmm", st);
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) {
+        st = bsmr_sddmm(plan, dA.p, dB.p, K, BSMR_F32, P, s);
+        if (st) die("bsmr_sddmm", st);
+    }
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    log.sddmmTime = ms / iters;
+    const double bytes = 4.0 * K * (static_cast<double>(M) + N) + 8.0 * nnz + 4.0 * (M + 1.0);
+    log.hbmGBs = static_cast<float>(bytes / (log.sddmmTime * 1e-3) / 1e9);
+    if (P_out) {
+        P_out->resize(nnz);
+        HIPCHK(hipMemcpy(P_out->data(), P, static_cast<size_t>(nnz) * 4, hipMemcpyDeviceToHost));
+    }
+    HIPCHK(hipEventDestroy(e0));
+    HIPCHK(hipEventDestroy(e1));
+    HIPCHK(hipStreamDestroy(s));
+}
+
+void fill_plan_fields(bsmr_plan* plan, uint32_t K, cli::Logger& log) {
+    bsmr_plan_stats ps;
+    bsmr_plan_get_stats(plan, &ps);
+    log.numRowPanels = static_cast<int>(ps.num_row_panels);
+    log.numClusters = ps.num_clusters;
+    log.rowReorderingTime = ps.row_reorder_ms;
+    log.colReorderingTime = ps.col_reorder_ms;
+    log.reorderingTime = ps.row_reorder_ms + ps.col_reorder_ms;
+    // launch-shape fields in the reference's terms (sddmmKernel.cu:2548-2553, 2570-2576, 2616-2618,
+    // 2733-2735): dense grid = panels x ceil(maxTiles/4), 128 threads; sparse grid = residual
+    // thread blocks (K > 32) or panels (K <= 32), 256 threads
+    log.gridDense = {ps.num_row_panels,
+                     static_cast<uint32_t>(std::ceil(static_cast<float>(ps.max_dense_tiles_per_panel) / 4)), 1};
+    log.blockDense = {128, 1, 1};
+    log.gridSparse = {K <= 32 ? ps.num_row_panels : ps.num_sparse_thread_blocks, 1, 1};
+    log.blockSparse = {256, 1, 1};
+    log.denseItems = ps.dense_items;
+    log.residualItems = ps.residual_items;
+    bsmr_eval_stats ev;
+    bsmr_plan_evaluate(plan, &ev);
+    log.numDenseBlock = ev.num_dense_block;
+    log.averageDensity = ev.average_density;
+    log.originalNumDenseBlock = ev.original_num_dense_block;
+    log.originalAverageDensity = ev.original_average_density;
+    log.numDenseThreadBlocks = static_cast<int>(ps.num_dense_thread_blocks);
+    log.numSparseThreadBlocks = static_cast<int>(ps.num_sparse_thread_blocks);
+    log.numDenseData = ev.num_dense_data;
+    log.numSparseData = ev.num_sparse_data;
+}
+
+void base_fields(const cli::Options& o, const bsmr_csr* S, uint32_t K, cli::Logger& log) {
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceProperties(&prop, 0) == hipSuccess) log.gpu = prop.name;
+    log.inputFile = o.inputFile();
+    uint32_t M, N, nnz;
+    bsmr_csr_info(S, &M, &N, &nnz);
+    log.M = M;
+    log.N = N;
+    log.NNZ = nnz;
+    const uint64_t total = static_cast<uint64_t>(M) * N;
+    log.sparsity = total == 0 ? 0.0f : 1.0f - static_cast<float>(nnz) / static_cast<float>(total);
+    log.K = K;
+    log.numITER = o.numIterations();
+    log.alpha = o.alpha();
+    log.delta = o.delta();
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    cli::Options options(argc, argv);
+    bsmr_csr* S = nullptr;
+    if (bsmr_csr_load_mtx(options.inputFile().c_str(), 1, &S) != BSMR_OK) {
+        fprintf(stderr, "Error, matrix S initialize failed.\n");
+        return -1;
+    }
+    uint32_t M, N, nnz;
+    bsmr_csr_info(S, &M, &N, &nnz);
+
+    if (options.testMode()) {  // sddmm_testMode (sddmm.cu:62-118)
+        const float alphas[] = {0.1f, 0.3f, 0.5f, 0.7f, 0.9f};
+        const float deltas[] = {0.0f, 0.1f, 0.3f, 0.5f, 0.7f, 0.9f, 1.1f};
+        const uint32_t Ks[] = {32, 64, 128, 256};
+        for (float alpha : alphas) {
+            bsmr_plan_options po;
+            bsmr_plan_options_default(&po);
+            po.alpha = alpha;
+            po.delta = deltas[0];
+            bsmr_plan* plan = nullptr;
+            int st = bsmr_plan_create(bsmr_csr_rowptr(S), bsmr_csr_colidx(S), M, N, nnz, &po, &plan);
+            if (st) die("bsmr_plan_create", st);
+            for (float delta : deltas) {
+                st = bsmr_plan_recolumn(plan, delta);
+                if (st) die("bsmr_plan_recolumn", st);
+                for (uint32_t k : Ks) {
+                    cli::Logger log;
+                    base_fields(options, S, k, log);
+                    log.alpha = alpha;
+                    log.delta = delta;
+                    fill_plan_fields(plan, k, log);
+                    run_sddmm(plan, S, k, options.numIterations(), log, nullptr);
+                    const std::string file = options.outputLogDirectory() + "BSMR_" + "k_" +
+                                             cli::to_trimmed_string(k) + "_" + "a_" +
+                                             cli::to_trimmed_string(alpha) + "_" + "d_" +
+                                             cli::to_trimmed_string(delta) + ".log";
+                    std::ofstream fout(file, std::ios::app);
+                    if (fout.fail()) {
+                        fprintf(stderr, "Error, failed to open log file: %s\n", file.c_str());
+                        bsmr_plan_destroy(plan);
+                        bsmr_csr_free(S);
+                        return 0;
+                    }
+                    fout << "\n---New data---\n";
+                    log.print(fout);
+                }
+            }
+            bsmr_plan_destroy(plan);
+        }
+        bsmr_csr_free(S);
+        return 0;
+    }
+
+    const uint32_t K = static_cast<uint32_t>(options.K());
+    cli::Logger log;
+    base_fields(options, S, K, log);
+    bsmr_plan_options po;
+    bsmr_plan_options_default(&po);
+    po.alpha = options.alpha();
+    po.delta = options.delta();
+    bsmr_plan* plan = nullptr;
+    int st = bsmr_plan_create(bsmr_csr_rowptr(S), bsmr_csr_colidx(S), M, N, nnz, &po, &plan);
+    if (st) die("bsmr_plan_create", st);
+    fill_plan_fields(plan, K, log);
+    run_sddmm(plan, S, K, options.numIterations(), log, nullptr);
+    log.print();
+    bsmr_plan_destroy(plan);
+    bsmr_csr_free(S);
+    return 0;
+}

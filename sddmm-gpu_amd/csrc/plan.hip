@@ -1,0 +1,976 @@
+// plan.hip — BSMR reordering and tile layout, built on the GPU (gfx950).
+//
+// Pipeline (reference functions in brackets; file:line relative to the reference root):
+//   1. k_encode        per-row LDS histogram of col/bs -> sparse encoding, dispersion, norms
+//                      [kernel::calculateDispersion, rowReordering.cu:49-93, 478-501]
+//   2. radix sort      rows stably by dispersion [host::sort_by_key, rowReordering.cu:1055-1062]
+//   3. k_cluster       similarity clustering as a persistent chain of wave-sized workgroups
+//                      [bsa_clustering + get_permutation_gpu, rowReordering.cu:215-432, 893-1007]
+//   4. radix sort      positions stably by cluster id -> reorderedRows [rowReordering.cu:988-996,
+//                      1081-1090]
+//   5. k_gather + segmented radix sort + k_panel_pass1/2: per-16-row-panel column histogram,
+//                      count-descending order, dense/sparse split and the RPHM tile/residual
+//                      arrays [colReordering_cpu, colReordering.cu:244-404; RPHM::RPHM,
+//                      BSMR.cpp:83-265]
+//   6. k_items         compact work lists for the SDDMM launch (replaces the reference's 2-D
+//                      panels x maxBlocks grid, sddmmKernel.cu:2570-2581)
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+#include "plan.hpp"
+#include "plan_kernels.hpp"
+
+namespace bsmr {
+namespace {
+
+using namespace dev;
+
+// ------------------------------------------------------------------------------------------
+// 1. Row encodings. One 256-thread workgroup per row: LDS histogram over the nbpr column
+// blocks, then an ordered compaction (ascending block id) into enc[rowptr[r] ...] as
+// (count << 16 | block). Also: #blocks, dispersion (u32, as the reference's sum), and the
+// "kept" integer norms used by the clustering similarity.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool kept_idx(u32 i, u32 B, u32 keptMask) {
+    return (keptMask >> ((i % B) >> 5)) & 1u;
+}
+
+__global__ __launch_bounds__(256) void k_encode(const u32* __restrict__ rowptr,
+                                                const u32* __restrict__ col, u32 M, u32 bs,
+                                                u32 nbpr, u32 B, u32 keptMask,
+                                                u32* __restrict__ enc, u32* __restrict__ nblk,
+                                                u32* __restrict__ disp, u32* __restrict__ SC,
+                                                u32* __restrict__ S1C) {
+    extern __shared__ __attribute__((aligned(16))) u32 smem[];
+    u32* hist = smem;                 // nbpr
+    u32* red = smem + ((nbpr + 3) & ~3u);  // 4 waves x 4 values
+    const u32 r = blockIdx.x;
+    const u32 t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const u32 b0 = rowptr[r], n = rowptr[r + 1] - b0;
+    if (n == 0) {
+        if (t == 0) {
+            nblk[r] = 0;
+            disp[r] = 0;
+            SC[r] = 0;
+            S1C[r] = 0;
+        }
+        return;
+    }
+    for (u32 i = t; i < nbpr; i += 256) hist[i] = 0;
+    __syncthreads();
+    for (u32 k = t; k < n; k += 256) atomicAdd(&hist[col[b0 + k] / bs], 1u);
+    __syncthreads();
+    const u32 chunk = (nbpr + 255) / 256;
+    const u32 i0 = min(t * chunk, nbpr), i1 = min(i0 + chunk, nbpr);
+    u32 cnz = 0, dsum = 0, sq = 0, s1 = 0;
+    for (u32 i = i0; i < i1; ++i) {
+        const u32 e = hist[i];
+        if (e) {
+            ++cnz;
+            dsum += bs - e;
+            if (kept_idx(i, B, keptMask)) {
+                sq += e * e;
+                s1 += e;
+            }
+        }
+    }
+    const u32 incl = wave_incl_scan(cnz);
+    const u32 wd = wave_sum(dsum), wq = wave_sum(sq), ws = wave_sum(s1);
+    if (lane == 63) {
+        red[w * 4 + 0] = incl;
+        red[w * 4 + 1] = wd;
+        red[w * 4 + 2] = wq;
+        red[w * 4 + 3] = ws;
+    }
+    __syncthreads();
+    u32 base = 0, tot = 0;
+    for (u32 j = 0; j < 4; ++j) {
+        if (j < w) base += red[j * 4];
+        tot += red[j * 4];
+    }
+    u32 off = b0 + base + incl - cnz;
+    for (u32 i = i0; i < i1; ++i) {
+        const u32 e = hist[i];
+        if (e) enc[off++] = (e << 16) | i;
+    }
+    if (t == 0) {
+        u32 d = 0, q = 0, s = 0;
+        for (u32 j = 0; j < 4; ++j) {
+            d += red[j * 4 + 1];
+            q += red[j * 4 + 2];
+            s += red[j * 4 + 3];
+        }
+        nblk[r] = tot;
+        disp[r] = d + n * tot;  // sum_{b}(bs - e_b) + nnz * #b, u32 wrap like the reference
+        SC[r] = q;
+        S1C[r] = s;
+    }
+}
+
+__global__ void k_iota(u32* p, u32 n) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = i;
+}
+
+// number of leading zeros in the sorted dispersion keys = number of empty rows
+__global__ void k_count_zero(const u32* __restrict__ sorted, u32 M, u32* out) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < M && sorted[i] == 0 && (i + 1 == M || sorted[i + 1] != 0)) *out = i + 1;
+}
+
+// state[pos] = ASSIGNED|0 for empty rows (cluster 0, rowReordering.cu:939-949), else 0 =
+// "rejected by virtual cluster 0"; st[0] = z + 1 so cluster 1 scans from position z.
+__global__ void k_init_state(u32* state, u32* st, u32 M, u32 z) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < M) state[i] = i < z ? ASSIGNED : 0u;
+    if (i == 0) st[0] = z + 1;
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. Clustering. The reference runs one single-block kernel per cluster and chains them with
+// per-row device mutexes and device-side launches; the result is sequential first-fit (cluster
+// c examines position i only after c-1 has). Here every cluster is one wave-sized workgroup of
+// a persistent launch; cluster k follows cluster k-1 through the per-position state word:
+//     state[i] = ASSIGNED | c   row assigned to cluster c (sticky)
+//     state[i] = c              unassigned, rejected by clusters 1..c
+// and k-1 publishes its start in st[k-1] (start + 2; ST_NONE = no such cluster). A launch runs
+// `R` consecutive clusters; the next launch continues from the last one's start.
+//
+// Similarity: calculate_similarity_norm_weighted_jaccard (rowReordering.cu:235-293) with the
+// reference's reduce_sum tree (cudaUtil.cuh:13-45) for block size B: each logical thread t<B
+// sums i = t, t+B, ... in order; xor-butterfly inside 32-lane warps; then the strided warp
+// tree that drops warps when B/32 is not a power of two (keptMask). The integer norms are kept
+// incrementally (u32 wrap, order-free). A double-precision estimate from the sparse row decides
+// whenever it is further than GUARD from alpha (fp32 tree error < 3e-6); otherwise
+// the exact fp32 emulation below decides.
+// ------------------------------------------------------------------------------------------
+struct ClusterArgs {
+    const u32* asc;
+    const u32* rowptr;  // encoding offsets (= CSR row offsets)
+    const u32* nblk;
+    const u32* enc;
+    const u32* SC;
+    const u32* S1C;
+    u32* state;
+    u32* st;
+    u32* ctrl;          // [0] abort, [1] timeout, [2..3] exact evals (u64), [4..5] total evals
+    u32 M, nbpr, B, keptMask, c0;
+    float alpha;
+    int exact_all;
+    u64 timeout_ticks;  // s_memrealtime ticks (100 MHz)
+};
+
+constexpr double GUARD = 1e-5;
+
+__device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+// exact fp32 similarity, all 64 lanes, rep/cmp dense in LDS
+__device__ float sim_exact(const u32* rep, const u32* cmp, u32 nbpr, u32 B, u32 keptMask,
+                           float nr, float nc, float* smn, float* smx) {
+    const u32 l = lane_id();
+    const u32 J = (B + 63) / 64;
+    for (u32 j = 0; j < J; ++j) {
+        const u32 t = l + 64 * j;
+        float pm = 0.0f, px = 0.0f;
+        if (t < B) {
+            for (u32 i = t; i < nbpr; i += B) {
+                const float x = static_cast<float>(rep[i]) / nr;
+                const float y = static_cast<float>(cmp[i]) / nc;
+                pm = pm + fminf(x, y);
+                px = px + fmaxf(x, y);
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            pm = pm + __shfl_xor(pm, o);
+            px = px + __shfl_xor(px, o);
+        }
+        if ((l & 31) == 0 && t < B) {
+            smn[t >> 5] = pm;
+            smx[t >> 5] = px;
+        }
+    }
+    __syncthreads();
+    float sim = 0.0f;
+    if (l == 0) {
+        for (u32 stride = B / 64; stride >= 1; stride >>= 1)
+            for (u32 w = 0; w < stride; ++w) {
+                smn[w] = smn[w] + smn[w + stride];
+                smx[w] = smx[w] + smx[w + stride];
+            }
+        sim = smn[0] / smx[0];
+    }
+    __syncthreads();
+    (void)keptMask;
+    return __shfl(sim, 0);
+}
+
+__global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) u32 smem[];
+    u32* rep = smem;                               // nbpr
+    u32* cmp = smem + ((a.nbpr + 3) & ~3u);        // nbpr (exact path only)
+    float* smn = reinterpret_cast<float*>(cmp + ((a.nbpr + 3) & ~3u));  // 32
+    float* smx = smn + 32;
+    __shared__ u32 s_abort;
+    const u32 l = lane_id();
+    const u32 k = a.c0 + blockIdx.x;
+    const u32 M = a.M;
+    u64 nexact = 0, ntotal = 0;
+    bool aborted = false;
+
+    auto check_abort = [&](u64 t_start) -> bool {
+        u32 ab = 0;
+        if (l == 0) {
+            ab = ld_agent(&a.ctrl[0]);
+            if (!ab && now_ticks() - t_start > a.timeout_ticks) {
+                st_agent(&a.ctrl[1], 1u);
+                st_agent(&a.ctrl[0], 1u);
+                ab = 1;
+            }
+        }
+        return __shfl(ab, 0) != 0;
+    };
+
+    // ---- wait for the predecessor's start
+    u32 sprev = 0;
+    {
+        const u64 t0 = now_ticks();
+        while (true) {
+            u32 v = 0;
+            if (l == 0) v = ld_agent(&a.st[k - 1]);
+            v = __shfl(v, 0);
+            if (v != 0) {
+                sprev = v;
+                break;
+            }
+            if (check_abort(t0)) return;
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+    if (sprev == ST_NONE) {
+        if (l == 0) st_agent(&a.st[k], ST_NONE);
+        return;
+    }
+    const u32 pred = k - 1;
+
+    // ---- find the start: first position after the predecessor's start rejected by it
+    u32 i = sprev - 1;
+    u32 start = M;
+    {
+        u64 t0 = now_ticks();
+        while (i < M) {
+            const u32 idx = i + l;
+            const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
+            const bool ready = (v & ASSIGNED) || v == pred;
+            const u64 notready = __ballot(!ready);
+            const u32 L = notready ? __builtin_ctzll(notready) : 64u;
+            const u64 cand = __ballot(ready && !(v & ASSIGNED) && l < L);
+            if (cand) {
+                start = i + __builtin_ctzll(cand);
+                break;
+            }
+            if (L == 0) {
+                if (check_abort(t0)) {
+                    aborted = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            } else {
+                i += L;
+                t0 = now_ticks();
+            }
+        }
+    }
+    if (aborted) return;
+    if (start >= M) {
+        if (l == 0) st_agent(&a.st[k], ST_NONE);
+        return;
+    }
+    if (l == 0) {
+        st_agent(&a.state[start], ASSIGNED | k);
+        st_agent(&a.st[k], start + 2);
+    }
+    // representative = encoding of the start row
+    for (u32 x = l; x < a.nbpr; x += 64) {
+        rep[x] = 0;
+        cmp[x] = 0;
+    }
+    __syncthreads();
+    u32 SR, SC0;
+    u64 S1R;
+    {
+        const u32 row = a.asc[start];
+        const u32 b0 = a.rowptr[row], nb = a.nblk[row];
+        for (u32 e = l; e < nb; e += 64) {
+            const u32 ent = a.enc[b0 + e];
+            rep[ent & 0xFFFFu] = ent >> 16;
+        }
+        SR = a.SC[row];
+        S1R = a.S1C[row];
+        (void)SC0;
+    }
+    __syncthreads();
+
+    // ---- main loop
+    i = start + 1;
+    u64 t0 = now_ticks();
+    while (i < M) {
+        const u32 idx = i + l;
+        const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
+        const bool ready = (v & ASSIGNED) || v == pred;
+        const u64 notready = __ballot(!ready);
+        const u32 L = notready ? __builtin_ctzll(notready) : 64u;
+        if (L == 0) {
+            if (check_abort(t0)) {
+                aborted = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        u64 todo = __ballot(!(v & ASSIGNED) && l < L);
+        while (todo) {
+            const u32 j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const u32 pos = i + j;
+            const u32 row = a.asc[pos];
+            const u32 b0 = a.rowptr[row], nb = a.nblk[row];
+            const u32 SCr = a.SC[row];
+            const u32 S1Cr = a.S1C[row];
+            ++ntotal;
+            bool accept;
+            if (SR == 0 && SCr == 0) {
+                accept = 1.0f > a.alpha;
+            } else if (SR == 0 || SCr == 0) {
+                accept = 0.0f > a.alpha;
+            } else {
+                const float nr = sqrtf(static_cast<float>(SR));
+                const float nc = sqrtf(static_cast<float>(SCr));
+                bool decided = false;
+                accept = false;
+                if (!a.exact_all) {
+                    double mn = 0.0;
+                    for (u32 e = l; e < nb; e += 64) {
+                        const u32 ent = a.enc[b0 + e];
+                        const u32 blk = ent & 0xFFFFu;
+                        const u32 rv = rep[blk];
+                        if (rv && kept_idx(blk, a.B, a.keptMask))
+                            mn += fmin(static_cast<double>(rv) / nr,
+                                       static_cast<double>(ent >> 16) / nc);
+                    }
+                    mn = wave_sum(mn);
+                    const double mx = static_cast<double>(S1R) / nr +
+                                      static_cast<double>(S1Cr) / nc - mn;
+                    const double sim = mn / mx;
+                    const double ad = static_cast<double>(a.alpha);
+                    if (fabs(sim - ad) > GUARD) {
+                        decided = true;
+                        accept = sim > ad;
+                    }
+                }
+                if (!decided) {
+                    ++nexact;
+                    for (u32 e = l; e < nb; e += 64) {
+                        const u32 ent = a.enc[b0 + e];
+                        cmp[ent & 0xFFFFu] = ent >> 16;
+                    }
+                    __syncthreads();
+                    const float sim = sim_exact(rep, cmp, a.nbpr, a.B, a.keptMask, nr, nc, smn, smx);
+                    accept = sim > a.alpha;
+                    for (u32 e = l; e < nb; e += 64) cmp[a.enc[b0 + e] & 0xFFFFu] = 0;
+                    __syncthreads();
+                }
+            }
+            if (accept) {
+                u32 dsr = 0, ds1 = 0;
+                for (u32 e = l; e < nb; e += 64) {
+                    const u32 ent = a.enc[b0 + e];
+                    const u32 blk = ent & 0xFFFFu, c = ent >> 16;
+                    const u32 o = rep[blk], nv = o + c;
+                    rep[blk] = nv;
+                    if (kept_idx(blk, a.B, a.keptMask)) {
+                        dsr += nv * nv - o * o;
+                        ds1 += c;
+                    }
+                }
+                SR += wave_sum(dsr);
+                S1R += wave_sum(ds1);
+                __syncthreads();
+            }
+            if (l == 0) st_agent(&a.state[pos], accept ? (ASSIGNED | k) : k);
+        }
+        i += L;
+        t0 = now_ticks();
+    }
+    (void)aborted;
+    (void)s_abort;
+    if (l == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[2]), nexact);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[4]), ntotal);
+    }
+}
+
+__global__ void k_ids(const u32* state, u32* ids, u32 M) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < M) ids[i] = state[i] & ~ASSIGNED;
+}
+
+// reorderedRows[q] = asc[indices[z + q]]
+__global__ void k_perm(const u32* asc, const u32* indices, u32 z, u32 R, u32* rows) {
+    const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < R) rows[q] = asc[indices[z + q]];
+}
+
+// ------------------------------------------------------------------------------------------
+// 5. Column split.
+// ------------------------------------------------------------------------------------------
+__global__ void k_row_nnz(const u32* rowptr, const u32* rows, u32 R, u32* rn) {
+    const u32 q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < R) rn[q] = rowptr[rows[q] + 1] - rowptr[rows[q]];
+}
+
+// one wave per reordered row: copy its columns into the panel segment (row order inside the
+// panel, file order inside the row, so a stable sort by column keeps row order per column)
+__global__ __launch_bounds__(256) void k_gather(const u32* __restrict__ rowptr,
+                                                const u32* __restrict__ col,
+                                                const u32* __restrict__ rows,
+                                                const u32* __restrict__ roff, u32 R,
+                                                u32* __restrict__ keys, u32* __restrict__ vals,
+                                                uint8_t* __restrict__ ent_lr,
+                                                u32* __restrict__ ent_idx) {
+    const u32 q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const u32 l = threadIdx.x & 63;
+    if (q >= R) return;
+    const u32 row = rows[q];
+    const u32 s = rowptr[row], n = rowptr[row + 1] - s, d = roff[q];
+    for (u32 j = l; j < n; j += 64) {
+        keys[d + j] = col[s + j];
+        vals[d + j] = d + j;
+        ent_lr[d + j] = static_cast<uint8_t>(q & 15u);
+        ent_idx[d + j] = s + j;
+    }
+}
+
+__global__ void k_segments(const u32* roff, u32 R, u32 P, u32* seg_begin, u32* seg_end) {
+    const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P) {
+        seg_begin[p] = roff[p * 16];
+        seg_end[p] = roff[min(p * 16 + 16, R)];
+    }
+}
+
+// F(x) = sum of counts over sorted positions < x, with hist[b] distinct columns of count 16-b
+// placed at bstart[b] (count-descending order).
+__device__ __forceinline__ u32 prefix_counts(u32 x, const u32* hist, const u32* bstart) {
+    u32 s = 0;
+#pragma unroll
+    for (u32 b = 0; b < 16; ++b) {
+        const u32 lo = bstart[b];
+        const u32 take = x > lo ? min(x - lo, hist[b]) : 0u;
+        s += take * (16u - b);
+    }
+    return s;
+}
+
+__device__ __forceinline__ u32 run_length(const u32* keys, u32 e, u32 end) {
+    const u32 key = keys[e];
+    u32 c = 1;
+    while (e + c < end && c < 16 && keys[e + c] == key) ++c;
+    return c;
+}
+
+// pass 1: per panel, count distinct columns per count bucket; dense groups; totals.
+__global__ __launch_bounds__(256) void k_panel_pass1(const u32* __restrict__ seg_begin,
+                                                     const u32* __restrict__ seg_end,
+                                                     const u32* __restrict__ skeys, u32 thr,
+                                                     u32* __restrict__ phist, u32* __restrict__ pnd,
+                                                     u32* __restrict__ pns, u32* __restrict__ psd) {
+    __shared__ u32 hist[16], bstart[16], dense_cnt;
+    const u32 p = blockIdx.x, t = threadIdx.x;
+    const u32 s0 = seg_begin[p], s1 = seg_end[p];
+    if (t < 16) hist[t] = 0;
+    if (t == 0) dense_cnt = 0;
+    __syncthreads();
+    for (u32 e = s0 + t; e < s1; e += 256) {
+        const bool head = e == s0 || skeys[e - 1] != skeys[e];
+        if (head) atomicAdd(&hist[16 - run_length(skeys, e, s1)], 1u);
+    }
+    __syncthreads();
+    if (t == 0) {
+        u32 acc = 0;
+        for (u32 b = 0; b < 16; ++b) {
+            bstart[b] = acc;
+            acc += hist[b];
+        }
+    }
+    __syncthreads();
+    const u32 ndist = bstart[15] + hist[15];
+    const u32 L = (ndist + 15) & ~15u;
+    u32 dense = 0;
+    for (u32 g = t; g < L / 16; g += 256) {
+        const u32 sum = prefix_counts(16 * g + 16, hist, bstart) - prefix_counts(16 * g, hist, bstart);
+        if (sum >= thr) ++dense;
+    }
+    dense = wave_sum(dense);
+    if ((t & 63) == 0 && dense) atomicAdd(&dense_cnt, dense);
+    __syncthreads();
+    if (t < 16) phist[p * 16 + t] = hist[t];
+    if (t == 0) {
+        const u32 nd = 16 * dense_cnt;
+        pnd[p] = nd;
+        pns[p] = L - nd;
+        psd[p] = (s1 - s0) - prefix_counts(nd, hist, bstart);
+    }
+}
+
+// pass 2: rank every distinct column inside its count bucket (column-ascending), place it,
+// and scatter its entries into the dense tiles or the residual lists.
+__global__ __launch_bounds__(256) void k_panel_pass2(
+    const u32* __restrict__ seg_begin, const u32* __restrict__ seg_end,
+    const u32* __restrict__ skeys, const u32* __restrict__ svals,
+    const uint8_t* __restrict__ ent_lr, const u32* __restrict__ ent_idx,
+    const u32* __restrict__ phist, const u32* __restrict__ pnd,
+    const u32* __restrict__ dcoff, const u32* __restrict__ scoff, const u32* __restrict__ sdoff,
+    u32 N, u32* __restrict__ denseCols, u32* __restrict__ sparseCols,
+    u32* __restrict__ blockValues, u32* __restrict__ sparseValues,
+    u32* __restrict__ sparseRel, u32* __restrict__ sparseColIdx) {
+    __shared__ u32 hist[16], bstart[16], base[16], wcnt[4][16];
+    const u32 p = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const u32 s0 = seg_begin[p], s1 = seg_end[p];
+    if (t < 16) {
+        hist[t] = phist[p * 16 + t];
+        base[t] = 0;
+    }
+    __syncthreads();
+    if (t == 0) {
+        u32 acc = 0;
+        for (u32 b = 0; b < 16; ++b) {
+            bstart[b] = acc;
+            acc += hist[b];
+        }
+    }
+    __syncthreads();
+    const u32 nd = pnd[p];
+    const u32 dOff = dcoff[p], sOff = scoff[p], sdOff = sdoff[p];
+    const u64 tile0 = dcoff[p] / 16;
+    const u32 Fnd = prefix_counts(nd, hist, bstart);
+    const u64 lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (u32 c0 = s0; c0 < s1; c0 += 256) {
+        const u32 e = c0 + t;
+        bool head = false;
+        u32 b = 0, c = 0;
+        if (e < s1) {
+            head = e == s0 || skeys[e - 1] != skeys[e];
+            if (head) {
+                c = run_length(skeys, e, s1);
+                b = 16 - c;
+            }
+        }
+        u32 rank = 0;
+#pragma unroll
+        for (u32 bb = 0; bb < 16; ++bb) {
+            const u64 m = __ballot(head && b == bb);
+            if (head && b == bb) rank = __popcll(m & lt);
+            if (lane == 0) wcnt[w][bb] = __popcll(m);
+        }
+        __syncthreads();
+        if (head) {
+            for (u32 j = 0; j < w; ++j) rank += wcnt[j][b];
+            rank += base[b];
+            const u32 pos = bstart[b] + rank;
+            const u32 colv = skeys[e];
+            if (pos < nd) {
+                denseCols[dOff + pos] = colv;
+                const u64 tb = (tile0 + pos / 16) * 256ull + (pos % 16);
+                for (u32 j = 0; j < c; ++j) {
+                    const u32 ent = svals[e + j];
+                    blockValues[tb + 16ull * ent_lr[ent]] = ent_idx[ent];
+                }
+            } else {
+                sparseCols[sOff + pos - nd] = colv;
+                const u32 rb = sdOff + prefix_counts(pos, hist, bstart) - Fnd;
+                for (u32 j = 0; j < c; ++j) {
+                    const u32 ent = svals[e + j];
+                    sparseValues[rb + j] = ent_idx[ent];
+                    sparseRel[rb + j] = ent_lr[ent];
+                    sparseColIdx[rb + j] = colv;
+                }
+            }
+        }
+        __syncthreads();
+        if (t < 16) {
+            u32 s = 0;
+            for (u32 j = 0; j < 4; ++j) s += wcnt[j][t];
+            base[t] += s;
+        }
+        __syncthreads();
+    }
+    // sentinel padding (column N) up to a multiple of 16 (colReordering.cu:338-343)
+    const u32 ndist = bstart[15] + hist[15];
+    const u32 L = (ndist + 15) & ~15u;
+    for (u32 pos = ndist + t; pos < L; pos += 256) {
+        if (pos < nd)
+            denseCols[dOff + pos] = N;
+        else
+            sparseCols[sOff + pos - nd] = N;
+    }
+}
+
+__global__ void k_div16(const u32* in, u32* out, u32 n) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i] / 16;
+}
+
+// ------------------------------------------------------------------------------------------
+// 6. Work lists: dense items {panel, first tile, tiles} of <= TILES_PER_ITEM tiles, residual
+// items {panel, first entry, end entry} of <= RES_PER_ITEM entries.
+// ------------------------------------------------------------------------------------------
+__global__ void k_item_counts(const u32* pnd, const u32* psd, u32 P, u32 tpi, u32 rpi, u32* dc,
+                              u32* rc) {
+    const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P) {
+        dc[p] = (pnd[p] / 16 + tpi - 1) / tpi;
+        rc[p] = (psd[p] + rpi - 1) / rpi;
+    }
+}
+
+__global__ void k_item_fill(const u32* dcoff, const u32* sdoff, const u32* doffs,
+                            const u32* roffs, u32 P, u32 tpi, u32 rpi, uint4* ditems,
+                            uint4* ritems) {
+    const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const u32 t0 = dcoff[p] / 16, t1 = dcoff[p + 1] / 16;
+    u32 o = doffs[p];
+    for (u32 t = t0; t < t1; t += tpi) ditems[o++] = make_uint4(p, t, min(tpi, t1 - t), 0);
+    const u32 e0 = sdoff[p], e1 = sdoff[p + 1];
+    o = roffs[p];
+    for (u32 e = e0; e < e1; e += rpi) ritems[o++] = make_uint4(p, e, min(e + rpi, e1), 0);
+}
+
+inline u32 grid_for(u64 n, u32 b) { return static_cast<u32>((n + b - 1) / b); }
+
+// exclusive scan of n values into out[0..n] (out[n] = total)
+int excl_scan(const u32* in, u32* out, u32 n, DevBuf<uint8_t>& tmp, hipStream_t s) {
+    BSMR_HIP(hipMemsetAsync(out, 0, sizeof(u32), s));
+    if (n == 0) return BSMR_OK;
+    size_t bytes = 0;
+    BSMR_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out + 1, static_cast<int>(n), s));
+    if (bytes > tmp.size()) BSMR_CHECK(tmp.alloc(bytes));
+    BSMR_HIP(hipcub::DeviceScan::InclusiveSum(tmp.data(), bytes, in, out + 1, static_cast<int>(n), s));
+    return BSMR_OK;
+}
+
+int sort_pairs(const u32* kin, u32* kout, const u32* vin, u32* vout, u32 n, int end_bit,
+               DevBuf<uint8_t>& tmp, hipStream_t s) {
+    if (n == 0) return BSMR_OK;
+    size_t bytes = 0;
+    BSMR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout,
+                                                static_cast<int>(n), 0, end_bit, s));
+    if (bytes > tmp.size()) BSMR_CHECK(tmp.alloc(bytes));
+    BSMR_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.data(), bytes, kin, kout, vin, vout,
+                                                static_cast<int>(n), 0, end_bit, s));
+    return BSMR_OK;
+}
+
+template <typename T>
+int read_one(const T* dptr, T& h, hipStream_t s) {
+    BSMR_HIP(hipMemcpyAsync(&h, dptr, sizeof(T), hipMemcpyDeviceToHost, s));
+    BSMR_HIP(hipStreamSynchronize(s));
+    return BSMR_OK;
+}
+
+int bits_for(u64 maxval) {
+    int b = 1;
+    while (b < 32 && (1ull << b) <= maxval) ++b;
+    return b;
+}
+
+}  // namespace
+
+// calculateBlockSize (rowReordering.cu:1009-1025); free memory is an explicit input.
+u32 block_size_for(u32 M, u32 N, u64 free_mem) {
+    const u32 gmem = static_cast<u32>(std::ceil(static_cast<float>(static_cast<u64>(M) * M * 4ull) /
+                                                static_cast<float>(free_mem / 2)));
+    const u32 smem = static_cast<u32>(
+        std::ceil(static_cast<float>(static_cast<u64>(N) * 4ull) / static_cast<float>(REF_MAX_SHMEM / 2)));
+    const u32 bs = std::max(gmem, smem);
+    return bs > 16 ? bs : 16;
+}
+
+// bsa_clustering block size (rowReordering.cu:911-920)
+u32 cluster_block_dim(u32 nbpr) {
+    if (nbpr < 32) return 32;
+    int cand = static_cast<int>(32 * std::ceil(static_cast<float>(static_cast<int>(nbpr) / 4) / 32.0f));
+    cand = cand > 32 ? cand : 32;
+    return static_cast<u32>(1024 < cand ? 1024 : cand);
+}
+
+// warps whose partial sums reach s[0] in cuUtil::reduce_sum (cudaUtil.cuh:27-45)
+u32 kept_warp_mask(u32 B) {
+    const u32 W = B / 32;
+    std::vector<u32> reach(W);
+    for (u32 w = 0; w < W; ++w) reach[w] = 1u << w;
+    for (u32 stride = B / 64; stride >= 1; stride >>= 1)
+        for (u32 w = 0; w < stride; ++w) reach[w] |= reach[w + stride];
+    return reach[0];
+}
+
+int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
+    hipStream_t s = stream;
+    hipEvent_t e0, e1;
+    BSMR_HIP(hipEventCreate(&e0));
+    BSMR_HIP(hipEventCreate(&e1));
+    BSMR_CHECK(rowptr.upload(h_rowptr, M + 1ull, s));
+    BSMR_CHECK(colidx.upload(h_col, nnz, s));
+    BSMR_HIP(hipEventRecord(e0, s));
+
+    // 1. encodings
+    BSMR_CHECK(enc.alloc(std::max<u32>(nnz, 1)));
+    BSMR_CHECK(nblk.alloc(M));
+    BSMR_CHECK(disp.alloc(M));
+    BSMR_CHECK(SC.alloc(M));
+    BSMR_CHECK(S1C.alloc(M));
+    const size_t lds_enc = (((nbpr + 3) & ~3u) + 16) * sizeof(u32);
+    hipLaunchKernelGGL(k_encode, dim3(M), dim3(256), lds_enc, s, rowptr.data(), colidx.data(), M,
+                       bs, nbpr, B, keptMask, enc.data(), nblk.data(), disp.data(), SC.data(),
+                       S1C.data());
+    BSMR_HIP(hipGetLastError());
+
+    // 2. ascending = rows stably sorted by dispersion
+    DevBuf<u32> keys_sorted, iota;
+    BSMR_CHECK(keys_sorted.alloc(M));
+    BSMR_CHECK(iota.alloc(M));
+    BSMR_CHECK(asc.alloc(M));
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(M, 256)), dim3(256), 0, s, iota.data(), M);
+    BSMR_CHECK(sort_pairs(disp.data(), keys_sorted.data(), iota.data(), asc.data(), M, 32, tmp, s));
+    DevBuf<u32> zdev;
+    BSMR_CHECK(zdev.alloc(1));
+    BSMR_HIP(hipMemsetAsync(zdev.data(), 0, sizeof(u32), s));
+    hipLaunchKernelGGL(k_count_zero, dim3(grid_for(M, 256)), dim3(256), 0, s, keys_sorted.data(), M,
+                       zdev.data());
+    BSMR_CHECK(read_one(zdev.data(), z, s));
+
+    // 3. clustering
+    DevBuf<u32> state, st, ctrl;
+    BSMR_CHECK(state.alloc(M));
+    BSMR_CHECK(st.alloc(M + 2ull));
+    BSMR_CHECK(ctrl.alloc(8));
+    BSMR_HIP(hipMemsetAsync(st.data(), 0, (M + 2ull) * sizeof(u32), s));
+    BSMR_HIP(hipMemsetAsync(ctrl.data(), 0, 8 * sizeof(u32), s));
+    hipLaunchKernelGGL(k_init_state, dim3(grid_for(M, 256)), dim3(256), 0, s, state.data(), st.data(),
+                       M, z);
+    BSMR_HIP(hipGetLastError());
+    ClusterArgs ca{};
+    ca.asc = asc.data();
+    ca.rowptr = rowptr.data();
+    ca.nblk = nblk.data();
+    ca.enc = enc.data();
+    ca.SC = SC.data();
+    ca.S1C = S1C.data();
+    ca.state = state.data();
+    ca.st = st.data();
+    ca.ctrl = ctrl.data();
+    ca.M = M;
+    ca.nbpr = nbpr;
+    ca.B = B;
+    ca.keptMask = keptMask;
+    ca.alpha = alpha;
+    ca.exact_all = exact_all;
+    ca.timeout_ticks = 100ull * 1000 * 1000 * 20;  // 20 s without progress
+    const size_t lds_cl = (2 * ((nbpr + 3) & ~3u) + 64) * sizeof(u32);
+    u32 c0 = 1;
+    u32 last_valid = 0;
+    while (c0 <= M) {  // at most M - z clusters
+        const u32 R = std::min<u32>(cluster_batch, M + 1 - c0);
+        ca.c0 = c0;
+        hipLaunchKernelGGL(k_cluster, dim3(R), dim3(64), lds_cl, s, ca);
+        BSMR_HIP(hipGetLastError());
+        std::vector<u32> hst(R);
+        BSMR_HIP(hipMemcpyAsync(hst.data(), st.data() + c0, R * sizeof(u32), hipMemcpyDeviceToHost, s));
+        u32 hctrl[8];
+        BSMR_HIP(hipMemcpyAsync(hctrl, ctrl.data(), sizeof(hctrl), hipMemcpyDeviceToHost, s));
+        BSMR_HIP(hipStreamSynchronize(s));
+        if (hctrl[0]) {
+            set_error("clustering kernel aborted (timeout waiting for predecessor)");
+            return BSMR_ERR_TIMEOUT;
+        }
+        bool done = false;
+        for (u32 j = 0; j < R; ++j) {
+            if (hst[j] == ST_NONE) {
+                done = true;
+                break;
+            }
+            last_valid = c0 + j;
+        }
+        exact_evals = (static_cast<u64>(hctrl[3]) << 32) | hctrl[2];
+        total_evals = (static_cast<u64>(hctrl[5]) << 32) | hctrl[4];
+        if (done) break;
+        c0 += R;
+    }
+    (void)last_valid;
+
+    // 4. stable sort of positions by cluster id
+    DevBuf<u32> ids, sorted_ids, indices;
+    BSMR_CHECK(ids.alloc(M));
+    BSMR_CHECK(sorted_ids.alloc(M));
+    BSMR_CHECK(indices.alloc(M));
+    hipLaunchKernelGGL(k_ids, dim3(grid_for(M, 256)), dim3(256), 0, s, state.data(), ids.data(), M);
+    BSMR_CHECK(sort_pairs(ids.data(), sorted_ids.data(), iota.data(), indices.data(), M,
+                          bits_for(M + 1ull), tmp, s));
+    R = M - z;
+    BSMR_CHECK(rows.alloc(std::max<u32>(R, 1)));
+    hipLaunchKernelGGL(k_perm, dim3(grid_for(R, 256)), dim3(256), 0, s, asc.data(), indices.data(), z,
+                       R, rows.data());
+    BSMR_HIP(hipGetLastError());
+    // numClusters = sorted_ids[indices[M-1]] + (zero rows ? 1 : 0) (rowReordering.cu:996)
+    u32 last_index = 0, id_at = 0;
+    BSMR_CHECK(read_one(indices.data() + (M - 1), last_index, s));
+    BSMR_CHECK(read_one(sorted_ids.data() + last_index, id_at, s));
+    numClusters = static_cast<int32_t>(id_at) + (z != 0 ? 1 : 0);
+    P = (R + 15) / 16;  // ceil(float(R)/16) (BSMR.cpp:48)
+
+    BSMR_HIP(hipEventRecord(e1, s));
+    BSMR_HIP(hipEventSynchronize(e1));
+    BSMR_HIP(hipEventElapsedTime(&row_ms, e0, e1));
+    BSMR_HIP(hipEventDestroy(e0));
+    BSMR_HIP(hipEventDestroy(e1));
+    // the encodings are only needed by the clustering
+    enc.release();
+    SC.release();
+    S1C.release();
+    return BSMR_OK;
+}
+
+int Plan::build_columns() {
+    hipStream_t s = stream;
+    hipEvent_t e0, e1;
+    BSMR_HIP(hipEventCreate(&e0));
+    BSMR_HIP(hipEventCreate(&e1));
+    BSMR_HIP(hipEventRecord(e0, s));
+    if (!segments_ready) {
+        DevBuf<u32> rn;
+        BSMR_CHECK(rn.alloc(std::max<u32>(R, 1)));
+        BSMR_CHECK(roff.alloc(R + 1ull));
+        hipLaunchKernelGGL(k_row_nnz, dim3(grid_for(R, 256)), dim3(256), 0, s, rowptr.data(),
+                           rows.data(), R, rn.data());
+        BSMR_CHECK(excl_scan(rn.data(), roff.data(), R, tmp, s));
+        DevBuf<u32> keys, vals;
+        BSMR_CHECK(keys.alloc(nnz));
+        BSMR_CHECK(vals.alloc(nnz));
+        BSMR_CHECK(skeys.alloc(nnz));
+        BSMR_CHECK(svals.alloc(nnz));
+        BSMR_CHECK(ent_lr.alloc(nnz));
+        BSMR_CHECK(ent_idx.alloc(nnz));
+        hipLaunchKernelGGL(k_gather, dim3(grid_for(R, 4)), dim3(256), 0, s, rowptr.data(),
+                           colidx.data(), rows.data(), roff.data(), R, keys.data(), vals.data(),
+                           ent_lr.data(), ent_idx.data());
+        BSMR_CHECK(seg_begin.alloc(P));
+        BSMR_CHECK(seg_end.alloc(P));
+        hipLaunchKernelGGL(k_segments, dim3(grid_for(P, 256)), dim3(256), 0, s, roff.data(), R, P,
+                           seg_begin.data(), seg_end.data());
+        BSMR_HIP(hipGetLastError());
+        size_t bytes = 0;
+        const int endbit = bits_for(N);
+        BSMR_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, bytes, keys.data(), skeys.data(), vals.data(), svals.data(),
+            static_cast<int>(nnz), static_cast<int>(P), seg_begin.data(), seg_end.data(), 0, endbit,
+            s));
+        if (bytes > tmp.size()) BSMR_CHECK(tmp.alloc(bytes));
+        BSMR_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            tmp.data(), bytes, keys.data(), skeys.data(), vals.data(), svals.data(),
+            static_cast<int>(nnz), static_cast<int>(P), seg_begin.data(), seg_end.data(), 0, endbit,
+            s));
+        segments_ready = true;
+    }
+    // pass 1
+    const u32 thr = static_cast<u32>(std::ceil(delta * static_cast<float>(TILE)));  // colReordering.cu:246
+    DevBuf<u32> phist, pnd, pns, psd;
+    BSMR_CHECK(phist.alloc(16ull * P));
+    BSMR_CHECK(pnd.alloc(P));
+    BSMR_CHECK(pns.alloc(P));
+    BSMR_CHECK(psd.alloc(P));
+    hipLaunchKernelGGL(k_panel_pass1, dim3(P), dim3(256), 0, s, seg_begin.data(), seg_end.data(),
+                       skeys.data(), thr, phist.data(), pnd.data(), pns.data(), psd.data());
+    BSMR_HIP(hipGetLastError());
+    BSMR_CHECK(denseColOffsets.alloc(P + 1ull));
+    BSMR_CHECK(sparseColOffsets.alloc(P + 1ull));
+    BSMR_CHECK(sparseValueOffsets.alloc(P + 1ull));
+    BSMR_CHECK(blockOffsets.alloc(P + 1ull));
+    BSMR_CHECK(excl_scan(pnd.data(), denseColOffsets.data(), P, tmp, s));
+    BSMR_CHECK(excl_scan(pns.data(), sparseColOffsets.data(), P, tmp, s));
+    BSMR_CHECK(excl_scan(psd.data(), sparseValueOffsets.data(), P, tmp, s));
+    hipLaunchKernelGGL(k_div16, dim3(grid_for(P + 1ull, 256)), dim3(256), 0, s, denseColOffsets.data(),
+                       blockOffsets.data(), P + 1);
+    u32 nDenseCols = 0, nSparseCols = 0;
+    BSMR_CHECK(read_one(denseColOffsets.data() + P, nDenseCols, s));
+    BSMR_CHECK(read_one(sparseColOffsets.data() + P, nSparseCols, s));
+    BSMR_CHECK(read_one(sparseValueOffsets.data() + P, nres, s));
+    numDenseTiles = nDenseCols / 16;
+    BSMR_CHECK(denseCols.alloc(std::max<u32>(nDenseCols, 1)));
+    BSMR_CHECK(sparseCols.alloc(std::max<u32>(nSparseCols, 1)));
+    BSMR_CHECK(blockValues.alloc(std::max<u64>(static_cast<u64>(numDenseTiles) * TILE, 1)));
+    BSMR_CHECK(sparseValues.alloc(std::max<u32>(nres, 1)));
+    BSMR_CHECK(sparseRel.alloc(std::max<u32>(nres, 1)));
+    BSMR_CHECK(sparseColIdx.alloc(std::max<u32>(nres, 1)));
+    denseCols.n = nDenseCols;
+    sparseCols.n = nSparseCols;
+    blockValues.n = static_cast<size_t>(numDenseTiles) * TILE;
+    sparseValues.n = sparseRel.n = sparseColIdx.n = nres;
+    if (blockValues.n)
+        BSMR_HIP(hipMemsetAsync(blockValues.data(), 0xFF, blockValues.n * sizeof(u32), s));
+    hipLaunchKernelGGL(k_panel_pass2, dim3(P), dim3(256), 0, s, seg_begin.data(), seg_end.data(),
+                       skeys.data(), svals.data(), ent_lr.data(), ent_idx.data(), phist.data(),
+                       pnd.data(), denseColOffsets.data(), sparseColOffsets.data(),
+                       sparseValueOffsets.data(), N, denseCols.data(), sparseCols.data(),
+                       blockValues.data(), sparseValues.data(), sparseRel.data(),
+                       sparseColIdx.data());
+    BSMR_HIP(hipGetLastError());
+
+    // 6. work lists
+    DevBuf<u32> dc, rc, doffs, roffs;
+    BSMR_CHECK(dc.alloc(P));
+    BSMR_CHECK(rc.alloc(P));
+    BSMR_CHECK(doffs.alloc(P + 1ull));
+    BSMR_CHECK(roffs.alloc(P + 1ull));
+    hipLaunchKernelGGL(k_item_counts, dim3(grid_for(P, 256)), dim3(256), 0, s, pnd.data(), psd.data(),
+                       P, TILES_PER_ITEM, RES_PER_ITEM, dc.data(), rc.data());
+    BSMR_CHECK(excl_scan(dc.data(), doffs.data(), P, tmp, s));
+    BSMR_CHECK(excl_scan(rc.data(), roffs.data(), P, tmp, s));
+    BSMR_CHECK(read_one(doffs.data() + P, nDenseItems, s));
+    BSMR_CHECK(read_one(roffs.data() + P, nResItems, s));
+    BSMR_CHECK(denseItems.alloc(std::max<u32>(nDenseItems, 1)));
+    BSMR_CHECK(resItems.alloc(std::max<u32>(nResItems, 1)));
+    hipLaunchKernelGGL(k_item_fill, dim3(grid_for(P, 256)), dim3(256), 0, s, denseColOffsets.data(),
+                       sparseValueOffsets.data(), doffs.data(), roffs.data(), P, TILES_PER_ITEM,
+                       RES_PER_ITEM, denseItems.data(), resItems.data());
+    BSMR_HIP(hipGetLastError());
+
+    // host copies of the small per-panel arrays (shard cost model, stats)
+    BSMR_CHECK(blockOffsets.download(h_blockOffsets, s));
+    BSMR_CHECK(sparseValueOffsets.download(h_sparseValueOffsets, s));
+    maxTilesPerPanel = 0;
+    numSparseTB = 0;
+    numDenseTB = 0;
+    for (u32 p = 0; p < P; ++p) {
+        const u32 nt = h_blockOffsets[p + 1] - h_blockOffsets[p];
+        maxTilesPerPanel = std::max(maxTilesPerPanel, nt);
+        numDenseTB += static_cast<u32>(std::ceil(static_cast<float>(nt) / REF_DENSE_BLOCKS_PER_TB));
+        numSparseTB += static_cast<u32>(std::ceil(
+            static_cast<float>(h_sparseValueOffsets[p + 1] - h_sparseValueOffsets[p]) /
+            REF_SPARSE_DATA_PER_TB));
+    }
+
+    BSMR_HIP(hipEventRecord(e1, s));
+    BSMR_HIP(hipEventSynchronize(e1));
+    BSMR_HIP(hipEventElapsedTime(&col_ms, e0, e1));
+    BSMR_HIP(hipEventDestroy(e0));
+    BSMR_HIP(hipEventDestroy(e1));
+    return BSMR_OK;
+}
+
+}  // namespace bsmr

@@ -1,0 +1,63 @@
+// plan.hpp — the device-resident BSMR plan (reference BSMR + RPHM, include/BSMR.hpp:21-159).
+#pragma once
+
+#include <vector>
+
+#include "common.hpp"
+
+namespace bsmr {
+
+// SDDMM work-list granularity
+constexpr u32 TILES_PER_ITEM = 4;   // dense tiles per wave item (A panel kept in registers)
+constexpr u32 RES_PER_ITEM = 256;   // residual entries per wave item
+
+u32 block_size_for(u32 M, u32 N, u64 free_mem);
+u32 cluster_block_dim(u32 nbpr);
+u32 kept_warp_mask(u32 B);
+
+struct Plan {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    u32 M = 0, N = 0, nnz = 0;
+    u32 bs = 16, nbpr = 1, B = 32, keptMask = 1;
+    float alpha = 0.3f, delta = 0.3f;
+    int exact_all = 0;
+    u32 cluster_batch = 512;
+
+    // input
+    DevBuf<u32> rowptr, colidx;
+    // row stage
+    DevBuf<u32> enc, nblk, disp, SC, S1C, asc;
+    DevBuf<u32> rows;  // reorderedRows_
+    u32 z = 0, R = 0, P = 0;
+    int32_t numClusters = 1;
+    u64 exact_evals = 0, total_evals = 0;
+    float row_ms = 0.f, col_ms = 0.f;
+
+    // column stage (the sorted panel segments do not depend on delta and are kept)
+    bool segments_ready = false;
+    DevBuf<u32> roff, skeys, svals, ent_idx, seg_begin, seg_end;
+    DevBuf<uint8_t> ent_lr;
+    DevBuf<u32> denseCols, denseColOffsets, sparseCols, sparseColOffsets, sparseValueOffsets;
+    DevBuf<u32> blockOffsets, blockValues, sparseValues, sparseRel, sparseColIdx;
+    u32 numDenseTiles = 0, nres = 0, maxTilesPerPanel = 0, numDenseTB = 0, numSparseTB = 0;
+    std::vector<u32> h_blockOffsets, h_sparseValueOffsets;
+
+    // work lists
+    DevBuf<uint4> denseItems, resItems;
+    u32 nDenseItems = 0, nResItems = 0;
+
+    DevBuf<uint8_t> tmp;  // scan/sort scratch
+
+    int build_rows(const u32* h_rowptr, const u32* h_col);
+    int build_columns();
+    ~Plan() {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+}  // namespace bsmr
+
+struct bsmr_plan {
+    bsmr::Plan p;
+};
