@@ -84,6 +84,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    try:
+        # Share torch's HIP runtime when torch is present: torch/lib/libamdhip64.so and
+        # /opt/rocm's carry the same SONAME but torch asks for the unversioned name, so loading
+        # ours first would put two HIP runtimes in the process.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise BsmrError(f"HIP extension not built: {LIB_PATH} is missing "
                         "(run `make -C sddmm-gpu_amd`)")

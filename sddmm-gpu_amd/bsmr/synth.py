@@ -65,12 +65,13 @@ SUITESPARSE_REBUILDS = {
 
 
 def random_rows(M, N, nnz_per_row, seed, zipf=None, empty_frac=0.0):
-    """Rows with (roughly) nnz_per_row distinct columns; Zipf-popular columns when zipf is set."""
+    """Rows with nnz_per_row distinct columns (Poisson around a scalar, or an explicit
+    per-row count array); Zipf-popular columns when zipf is set."""
     rng = np.random.default_rng(seed)
     if np.isscalar(nnz_per_row):
         counts = rng.poisson(nnz_per_row, size=M).clip(1, N)
     else:
-        counts = np.asarray(nnz_per_row)
+        counts = np.asarray(nnz_per_row).clip(0, N)
     if empty_frac > 0:
         counts[rng.random(M) < empty_frac] = 0
     if zipf is not None:
@@ -83,8 +84,7 @@ def random_rows(M, N, nnz_per_row, seed, zipf=None, empty_frac=0.0):
         if c == 0:
             continue
         if zipf is not None:
-            pick = rng.choice(N, size=min(N, int(c * 1.3) + 8), replace=True, p=w)
-            pick = np.unique(perm[pick])[:c]
+            pick = perm[rng.choice(N, size=c, replace=False, p=w)]
         else:
             pick = rng.choice(N, size=c, replace=False)
         rows.append(np.full(len(pick), r))
@@ -93,13 +93,21 @@ def random_rows(M, N, nnz_per_row, seed, zipf=None, empty_frac=0.0):
 
 
 def nips_like(seed=20250801):
-    """C1/C2 stand-in: 1,500 x 12,419, ~746k nnz, Zipf(1.1) column popularity."""
+    """C1/C2 stand-in: 1,500 x 12,419 with exactly 746,316 nnz (the UCI NIPS docword shape),
+    log-normal document lengths, Zipf(1.1) word popularity."""
     M, N, target = 1500, 12419, 746316
     rng = np.random.default_rng(seed)
-    # ragged document lengths around 497 words
     lens = rng.lognormal(mean=np.log(440), sigma=0.5, size=M)
-    lens = np.maximum(8, lens * (target / lens.sum())).astype(np.int64)
-    lens[: target - lens.sum()] += 1 if target > lens.sum() else 0
+    lens = np.clip(np.round(lens * (target / lens.sum())), 8, N // 2).astype(np.int64)
+    diff = target - int(lens.sum())
+    step = 1 if diff > 0 else -1
+    i = 0
+    while diff != 0:
+        j = i % M
+        if 8 <= lens[j] + step <= N // 2:
+            lens[j] += step
+            diff -= step
+        i += 1
     return random_rows(M, N, lens, seed + 1, zipf=1.1)
 
 
