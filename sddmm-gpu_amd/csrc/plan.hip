@@ -652,6 +652,39 @@ __global__ void k_item_fill(const u32* dcoff, const u32* sdoff, const u32* doffs
     for (u32 e = e0; e < e1; e += rpi) ritems[o++] = make_uint4(p, e, min(e + rpi, e1), 0);
 }
 
+// Column-major residual execution list: key = (col % 8) * N + col keeps each XCD bucket's
+// columns together (the launch deals bucket x to blocks b with b % 8 == x, so one XCD's L2 holds
+// 1/8 of B) and, within a column, the reference's panel-major entry order.
+__global__ __launch_bounds__(256) void k_cm_keys(const u32* __restrict__ sdoff,
+                                                 const u32* __restrict__ rows,
+                                                 const u32* __restrict__ sparseRel,
+                                                 const u32* __restrict__ sparseColIdx, u32 N,
+                                                 u32* __restrict__ keys, u32* __restrict__ vals,
+                                                 u32* __restrict__ rowOf) {
+    const u32 p = blockIdx.x;
+    const u32 e0 = sdoff[p], e1 = sdoff[p + 1];
+    for (u32 e = e0 + threadIdx.x; e < e1; e += 256) {
+        const u32 c = sparseColIdx[e];
+        keys[e] = (c % XCD_BUCKETS) * N + c;
+        vals[e] = e;
+        rowOf[e] = rows[p * 16 + sparseRel[e]];
+    }
+}
+
+__global__ void k_cm_gather(const u32* __restrict__ order, const u32* __restrict__ rowOf,
+                            const u32* __restrict__ sparseColIdx,
+                            const u32* __restrict__ sparseValues, const u32* __restrict__ skeys,
+                            u32 n, u32 N, u32* __restrict__ cmRow, u32* __restrict__ cmCol,
+                            u32* __restrict__ cmOut, u32* __restrict__ bucketCount) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 e = order[i];
+    cmRow[i] = rowOf[e];
+    cmCol[i] = sparseColIdx[e];
+    cmOut[i] = sparseValues[e];
+    if (i + 1 == n || skeys[i] / N != skeys[i + 1] / N) bucketCount[skeys[i] / N] = i + 1;
+}
+
 inline u32 grid_for(u64 n, u32 b) { return static_cast<u32>((n + b - 1) / b); }
 
 // exclusive scan of n values into out[0..n] (out[n] = total)
@@ -930,6 +963,54 @@ int Plan::build_columns() {
                        blockValues.data(), sparseValues.data(), sparseRel.data(),
                        sparseColIdx.data());
     BSMR_HIP(hipGetLastError());
+
+    // column-major residual execution list + XCD-interleaved slots
+    {
+        const u32 n = nres;
+        BSMR_CHECK(cmRow.alloc(std::max<u32>(n, 1)));
+        BSMR_CHECK(cmCol.alloc(std::max<u32>(n, 1)));
+        BSMR_CHECK(cmOut.alloc(std::max<u32>(n, 1)));
+        std::vector<u32> ends(XCD_BUCKETS, 0);
+        if (n) {
+            DevBuf<u32> keys, vals, skeys2, order, rowOf, bcount;
+            BSMR_CHECK(keys.alloc(n));
+            BSMR_CHECK(vals.alloc(n));
+            BSMR_CHECK(skeys2.alloc(n));
+            BSMR_CHECK(order.alloc(n));
+            BSMR_CHECK(rowOf.alloc(n));
+            BSMR_CHECK(bcount.alloc(XCD_BUCKETS));
+            BSMR_HIP(hipMemsetAsync(bcount.data(), 0, XCD_BUCKETS * sizeof(u32), s));
+            hipLaunchKernelGGL(k_cm_keys, dim3(P), dim3(256), 0, s, sparseValueOffsets.data(),
+                               rows.data(), sparseRel.data(), sparseColIdx.data(), N, keys.data(),
+                               vals.data(), rowOf.data());
+            BSMR_CHECK(sort_pairs(keys.data(), skeys2.data(), vals.data(), order.data(), n,
+                                  bits_for(static_cast<u64>(XCD_BUCKETS) * N), tmp, s));
+            hipLaunchKernelGGL(k_cm_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
+                               rowOf.data(), sparseColIdx.data(), sparseValues.data(),
+                               skeys2.data(), n, N, cmRow.data(), cmCol.data(), cmOut.data(),
+                               bcount.data());
+            BSMR_HIP(hipGetLastError());
+            BSMR_HIP(hipMemcpyAsync(ends.data(), bcount.data(), XCD_BUCKETS * sizeof(u32),
+                                    hipMemcpyDeviceToHost, s));
+            BSMR_HIP(hipStreamSynchronize(s));
+            for (u32 b = 1; b < XCD_BUCKETS; ++b) ends[b] = std::max(ends[b], ends[b - 1]);
+        }
+        u32 rmax = 0;
+        std::vector<u32> begins(XCD_BUCKETS, 0);
+        for (u32 b = 0; b < XCD_BUCKETS; ++b) {
+            begins[b] = b ? ends[b - 1] : 0;
+            rmax = std::max(rmax, (ends[b] - begins[b] + CM_PER_ITEM - 1) / CM_PER_ITEM);
+        }
+        nSlots = rmax * XCD_BUCKETS;
+        std::vector<uint2> slots(std::max<u32>(nSlots, 1), make_uint2(0, 0));
+        for (u32 b = 0; b < XCD_BUCKETS; ++b)
+            for (u32 j = 0; j < rmax; ++j) {
+                const u32 e0 = std::min(begins[b] + j * CM_PER_ITEM, ends[b]);
+                slots[j * XCD_BUCKETS + b] = make_uint2(e0, std::min(e0 + CM_PER_ITEM, ends[b]));
+            }
+        BSMR_CHECK(cmSlots.upload(slots.data(), slots.size(), s));
+        BSMR_HIP(hipStreamSynchronize(s));  // `slots` is pageable host memory
+    }
 
     // 6. work lists
     DevBuf<u32> dc, rc, doffs, roffs;

@@ -8,8 +8,10 @@
 namespace bsmr {
 
 // SDDMM work-list granularity
-constexpr u32 TILES_PER_ITEM = 4;   // dense tiles per wave item (A panel kept in registers)
-constexpr u32 RES_PER_ITEM = 256;   // residual entries per wave item
+constexpr u32 TILES_PER_ITEM = 1;   // dense tiles per wave item
+constexpr u32 RES_PER_ITEM = 256;   // residual entries per panel-major wave item (panel ranges)
+constexpr u32 CM_PER_ITEM = 64;     // residual entries per column-major wave item (full launch)
+constexpr u32 XCD_BUCKETS = 8;      // MI355X XCDs: column bucket c % 8 -> blocks b with b % 8
 
 u32 block_size_for(u32 M, u32 N, u64 free_mem);
 u32 cluster_block_dim(u32 nbpr);
@@ -46,6 +48,12 @@ struct Plan {
     // work lists
     DevBuf<uint4> denseItems, resItems;
     u32 nDenseItems = 0, nResItems = 0;
+    // column-major residual execution list (same entries as the reference residual arrays,
+    // ordered by (column % 8, column), stable): A row, column, output index; and the
+    // XCD-interleaved slots {e0, e1} of the full launch
+    DevBuf<u32> cmRow, cmCol, cmOut;
+    DevBuf<uint2> cmSlots;
+    u32 nSlots = 0;
 
     DevBuf<uint8_t> tmp;  // scan/sort scratch
 

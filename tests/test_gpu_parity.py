@@ -166,9 +166,19 @@ def test_panel_shards_cover_every_output(world):
         assert a1 == b0 and a0 <= a1
     A = make_data(M * K)
     B = make_data(N * K)
-    full = run_sddmm(plan, A, B, K, len(ci))
+    # the output buffer starts as NaN: every entry must be written exactly by its shard
     pieces = run_sddmm(plan, A, B, K, len(ci), panels=shards)
-    assert np.array_equal(full, pieces)
+    assert np.isfinite(pieces).all()
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
+    assert O.check_data(ref, pieces) == 0
+    # a single shard leaves the other shards' outputs untouched
+    p0, p1 = shards[world // 2]
+    part = run_sddmm(plan, A, B, K, len(ci), panels=[(p0, p1)])
+    rows = plan.array("reorderedRows")
+    mine = np.zeros(len(ci), bool)
+    for r in rows[p0 * 16: p1 * 16]:
+        mine[rp[r]:rp[r + 1]] = True
+    assert np.isfinite(part[mine]).all() and np.isnan(part[~mine]).all()
 
 
 def test_values_independent_of_layout_permutation():
