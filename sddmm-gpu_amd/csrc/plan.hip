@@ -652,6 +652,18 @@ __global__ void k_item_fill(const u32* dcoff, const u32* sdoff, const u32* doffs
     for (u32 e = e0; e < e1; e += rpi) ritems[o++] = make_uint4(p, e, min(e + rpi, e1), 0);
 }
 
+// A-row index of every dense tile row (NULLV past the last reordered row), so a dense-tile wave
+// needs one dependent round trip less (tile -> rows directly, not tile -> panel -> rows).
+__global__ void k_tile_rows(const uint4* __restrict__ items, u32 nitems,
+                            const u32* __restrict__ rows, u32 R, u32* __restrict__ tileRows) {
+    const u32 i = blockIdx.x * 16 + (threadIdx.x >> 4), r = threadIdx.x & 15;
+    if (i >= nitems) return;
+    const uint4 it = items[i];
+    const u32 q = it.x * 16 + r;
+    const u32 row = q < R ? rows[q] : NULLV;
+    for (u32 j = 0; j < it.z; ++j) tileRows[(it.y + j) * 16ull + r] = row;
+}
+
 // Column-major residual execution list: key = (col % 8) * N + col keeps each XCD bucket's
 // columns together (the launch deals bucket x to blocks b with b % 8 == x, so one XCD's L2 holds
 // 1/8 of B) and, within a column, the reference's panel-major entry order.
@@ -1029,6 +1041,11 @@ int Plan::build_columns() {
     hipLaunchKernelGGL(k_item_fill, dim3(grid_for(P, 256)), dim3(256), 0, s, denseColOffsets.data(),
                        sparseValueOffsets.data(), doffs.data(), roffs.data(), P, TILES_PER_ITEM,
                        RES_PER_ITEM, denseItems.data(), resItems.data());
+    BSMR_HIP(hipGetLastError());
+    BSMR_CHECK(tileRows.alloc(std::max<u64>(static_cast<u64>(numDenseTiles) * 16, 1)));
+    if (nDenseItems)
+        hipLaunchKernelGGL(k_tile_rows, dim3(grid_for(nDenseItems, 16)), dim3(256), 0, s,
+                           denseItems.data(), nDenseItems, rows.data(), R, tileRows.data());
     BSMR_HIP(hipGetLastError());
 
     // host copies of the small per-panel arrays (shard cost model, stats)

@@ -48,6 +48,7 @@ struct Plan {
     // work lists
     DevBuf<uint4> denseItems, resItems;
     u32 nDenseItems = 0, nResItems = 0;
+    DevBuf<u32> tileRows;  // [tile][16] A-row index of each tile row (NULLV = none)
     // column-major residual execution list (same entries as the reference residual arrays,
     // ordered by (column % 8, column), stable): A row, column, output index; and the
     // XCD-interleaved slots {e0, e1} of the full launch

@@ -32,9 +32,9 @@ struct SddmmArgs {
     const float* A;
     const float* B;
     float* P;
-    // dense tiles
-    const uint4* ditems;
+    // dense tiles [d0, d0 + nd) (one tile per wave)
     u32 d0, nd;
+    const u32* tileRows;
     const u32* rows;
     u32 R, N, K;
     const u32* denseCols;
@@ -58,57 +58,59 @@ __device__ __forceinline__ float dot4(f32x4 a, f32x4 b) {
     return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
 
-// ---- dense tiles, K = KT (KT = 0: runtime K, multiple of 16)
+// ---- one dense tile, K = KT (KT = 0: runtime K, multiple of 16). The tile's 16 A-row indices
+// (tileRows), its 16 columns and its 256 output indices depend only on the tile id, so the wave
+// has two dependent memory round trips: metadata, then A/B.
 template <int KT>
-__device__ __forceinline__ void dense_item(const SddmmArgs& a, const uint4 it) {
+__device__ __forceinline__ void dense_tile(const SddmmArgs& a, const u32 tile) {
     const u32 K = KT > 0 ? KT : a.K;
     const u32 l = __lane_id(), rr = l & 15, g = l >> 4;
-    const u32 q = it.x * 16 + rr;
-    const bool rvalid = q < a.R;
-    const float* arow = a.A + static_cast<size_t>(rvalid ? a.rows[q] : 0) * K + 4 * g;
-    for (u32 t = 0; t < it.z; ++t) {
-        const u32 tile = it.y + t;
-        const u32 c = a.denseCols[tile * 16 + rr];
-        const bool cvalid = c < a.N;
-        const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * K + 4 * g;
-        f32x4 acc = {0, 0, 0, 0};
-        if constexpr (KT > 0) {
-            // chunks of at most 8 k-steps (128 k): 16 float4 = 64 VGPRs of operands in flight
-            constexpr int NK = KT / 16;
-            constexpr int CH = NK < 8 ? NK : 8;
+    const u32 row = a.tileRows[tile * 16 + rr];
+    const u32 c = a.denseCols[tile * 16 + rr];
+    const u32* bvals = a.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
+    u32 idx[4];
 #pragma unroll
-            for (int k0 = 0; k0 < NK; k0 += CH) {
-                f32x4 av[CH], bv[CH];
+    for (int r = 0; r < 4; ++r) idx[r] = bvals[16 * r];
+    const bool rvalid = row != NULLV;
+    const bool cvalid = c < a.N;
+    const float* arow = a.A + static_cast<size_t>(rvalid ? row : 0) * K + 4 * g;
+    const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * K + 4 * g;
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};  // two chains halve the MFMA dependency
+    if constexpr (KT > 0) {
+        // chunks of at most 8 k-steps (128 k): 16 float4 = 64 VGPRs of operands in flight
+        constexpr int NK = KT / 16;
+        constexpr int CH = NK < 8 ? NK : 8;
 #pragma unroll
-                for (int kk = 0; kk < CH; ++kk) {
-                    av[kk] = rvalid ? ld4(arow + 16 * (k0 + kk)) : f32x4{0, 0, 0, 0};
-                    bv[kk] = cvalid ? ld4(bcol + 16 * (k0 + kk)) : f32x4{0, 0, 0, 0};
-                }
+        for (int k0 = 0; k0 < NK; k0 += CH) {
+            f32x4 av[CH], bv[CH];
 #pragma unroll
-                for (int kk = 0; kk < CH; ++kk) {
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].x, bv[kk].x, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].y, bv[kk].y, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].z, bv[kk].z, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].w, bv[kk].w, acc, 0, 0, 0);
-                }
+            for (int kk = 0; kk < CH; ++kk) {
+                av[kk] = rvalid ? ld4(arow + 16 * (k0 + kk)) : f32x4{0, 0, 0, 0};
+                bv[kk] = cvalid ? ld4(bcol + 16 * (k0 + kk)) : f32x4{0, 0, 0, 0};
             }
-        } else {
-            for (u32 k = 0; k < K; k += 16) {
-                const f32x4 av = rvalid ? ld4(arow + k) : f32x4{0, 0, 0, 0};
-                const f32x4 bv = cvalid ? ld4(bcol + k) : f32x4{0, 0, 0, 0};
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+#pragma unroll
+            for (int kk = 0; kk < CH; ++kk) {
+                f32x4& acc = (kk & 1) ? acc1 : acc0;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].x, bv[kk].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].y, bv[kk].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].z, bv[kk].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk].w, bv[kk].w, acc, 0, 0, 0);
             }
         }
-        const u32* bvals = a.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const u32 idx = bvals[16 * r];
-            if (idx != NULLV) a.P[idx] = acc[r];
+    } else {
+        for (u32 k = 0; k < K; k += 16) {
+            const f32x4 av = rvalid ? ld4(arow + k) : f32x4{0, 0, 0, 0};
+            const f32x4 bv = cvalid ? ld4(bcol + k) : f32x4{0, 0, 0, 0};
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc0, 0, 0, 0);
         }
     }
+    const f32x4 acc = acc0 + acc1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (idx[r] != NULLV) a.P[idx[r]] = acc[r];
 }
 
 template <int G>
@@ -118,54 +120,156 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
-// ---- column-major residual slot: G lanes per entry, U entries per lane in flight
-template <int KT, int G>
+// DPP helpers on 16-lane rows (VALU only, no LDS crossbar)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                 CTRL, 0xF, 0xF, false));
+}
+// sum over the 16 lanes of a row, every lane gets the total
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dppf<0x141>(v);  // row_half_mirror
+    v += dppf<0x140>(v);  // row_mirror
+    return v;
+}
+// value of lane N of the row, in every lane of the row (row_newbcast, gfx90a+)
+template <int N>
+__device__ __forceinline__ u32 row_bcast(u32 v) {
+    return static_cast<u32>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x150 + N, 0xF, 0xF,
+                                                         false));
+}
+
+template <int W>
+struct vec;
+template <>
+struct vec<4> {
+    typedef float __attribute__((ext_vector_type(4))) t;
+};
+template <>
+struct vec<2> {
+    typedef float __attribute__((ext_vector_type(2))) t;
+};
+template <>
+struct vec<1> {
+    typedef float t;
+};
+template <int W>
+__device__ __forceinline__ float vdot(typename vec<W>::t a, typename vec<W>::t b) {
+    if constexpr (W == 4)
+        return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    else if constexpr (W == 2)
+        return a.x * b.x + a.y * b.y;
+    else
+        return a * b;
+}
+
+// ---- column-major residual slot (K = KT known). One 16-lane row per entry: lane s holds the
+// W-float pieces s, s+16, ... of A[row] and B[col]. Each row takes a contiguous share of the
+// slot's entries (sorted by column); per batch of 16 entries the row loads the metadata once
+// (one entry per lane) and broadcasts entry i with row_newbcast:i. U entries are in flight per
+// lane; the B pieces are re-loaded only when the column changes (a column run costs one B read);
+// the 16-lane dot-product reduction is four DPP adds.
+template <int KT>
 __device__ __forceinline__ void residual_cm(const SddmmArgs& a, const uint2 sl) {
-    constexpr u32 EPI = 64 / G;
-    const u32 l = __lane_id(), sub = l % G, grp = l / G;
-    if constexpr (KT > 0) {
-        // 16-byte pieces per lane per operand (KT < 4G only in never-selected instantiations)
-        constexpr int NF = KT >= 4 * G ? KT / (4 * G) : 1;
-        constexpr int U = NF >= 8 ? 1 : 8 / NF;     // entries in flight per lane (<= 64 VGPRs)
-        for (u32 base = sl.x; base < sl.y; base += EPI * U) {
-            f32x4 av[U][NF], bv[U][NF];
-            u32 out[U];
-            bool ok[U];
+    constexpr int W = KT >= 64 ? 4 : KT / 16;
+    constexpr int NF = KT / (16 * W);
+    constexpr int U = NF >= 8 ? 1 : 8 / NF;
+    typedef typename vec<W>::t vt;
+    const u32 l = __lane_id(), sub = l & 15, grp = l >> 4;
+    const u32 n = sl.y - sl.x;
+    const u32 share = (n + 3) / 4;
+    const u32 gs = sl.x + min(grp * share, n), ge = sl.x + min(grp * share + share, n);
+    u32 curc = NULLV;
+    vt bcur[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) bcur[f] = vt{};
+    for (u32 base = gs; base < ge; base += 16) {
+        const u32 e = base + sub;
+        const bool okm = e < ge;
+        const u32 mrow = okm ? a.cmRow[e] : 0u;
+        const u32 mcol = okm ? a.cmCol[e] : NULLV;
+        const u32 mout = okm ? a.cmOut[e] : 0u;
+        const u32 nb = min(16u, ge - base);
+#pragma unroll
+        for (int i0 = 0; i0 < 16; i0 += U) {
+            if (static_cast<u32>(i0) >= nb) break;
+            vt av[U][NF], bv[U][NF];
+            u32 cc[U], oo[U];
+            bool ok[U], chg[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const u32 e = base + u * EPI + grp;
-                ok[u] = e < sl.y;
-                const u32 ee = ok[u] ? e : sl.x;
-                out[u] = a.cmOut[ee];
-                const float* ap = a.A + static_cast<size_t>(a.cmRow[ee]) * KT + 4 * sub;
-                const float* bp = a.B + static_cast<size_t>(a.cmCol[ee]) * KT + 4 * sub;
+                constexpr int dummy = 0;
+                (void)dummy;
+                u32 r;
+                switch (i0 + u) {  // compile-time lane index after unrolling
+#define BSMR_B(I)                    \
+    case I:                          \
+        r = row_bcast<I>(mrow);      \
+        cc[u] = row_bcast<I>(mcol);  \
+        oo[u] = row_bcast<I>(mout);  \
+        break;
+                    BSMR_B(0) BSMR_B(1) BSMR_B(2) BSMR_B(3) BSMR_B(4) BSMR_B(5) BSMR_B(6) BSMR_B(7)
+                    BSMR_B(8) BSMR_B(9) BSMR_B(10) BSMR_B(11) BSMR_B(12) BSMR_B(13) BSMR_B(14)
+                    BSMR_B(15)
+#undef BSMR_B
+                    default:
+                        r = 0;
+                        cc[u] = NULLV;
+                        oo[u] = 0;
+                }
+                ok[u] = static_cast<u32>(i0 + u) < nb;
+                const u32 prev = u ? cc[u - 1] : curc;
+                chg[u] = ok[u] && cc[u] != prev;
+                const float* ap = a.A + static_cast<size_t>(ok[u] ? r : 0) * KT + W * sub;
 #pragma unroll
-                for (int f = 0; f < NF; ++f) {
-                    av[u][f] = ld4(ap + 4 * G * f);
-                    bv[u][f] = ld4(bp + 4 * G * f);
+                for (int f = 0; f < NF; ++f)
+                    av[u][f] = *reinterpret_cast<const vt*>(ap + 16 * W * f);
+                if (chg[u]) {
+                    const float* bp = a.B + static_cast<size_t>(cc[u]) * KT + W * sub;
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+                        bv[u][f] = *reinterpret_cast<const vt*>(bp + 16 * W * f);
                 }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+                if (!chg[u]) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) bv[u][f] = u ? bv[u - 1][f] : bcur[f];
+                }
                 float acc = 0.f;
 #pragma unroll
-                for (int f = 0; f < NF; ++f) acc += dot4(av[u][f], bv[u][f]);
-                acc = group_sum<G>(acc);
-                if (sub == 0 && ok[u]) a.P[out[u]] = acc;
+                for (int f = 0; f < NF; ++f) acc += vdot<W>(av[u][f], bv[u][f]);
+                acc = row_sum16(acc);
+                if (sub == 0 && ok[u]) a.P[oo[u]] = acc;
             }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) {
+                    curc = cc[u];
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) bcur[f] = bv[u][f];
+                }
         }
-    } else {
-        for (u32 base = sl.x; base < sl.y; base += EPI) {
-            const u32 e = base + grp;
-            const bool ok = e < sl.y;
-            const u32 ee = ok ? e : sl.x;
-            const float* ap = a.A + static_cast<size_t>(a.cmRow[ee]) * a.K;
-            const float* bp = a.B + static_cast<size_t>(a.cmCol[ee]) * a.K;
-            float acc = 0.f;
-            for (u32 k = 4 * sub; k < a.K; k += 4 * G) acc += dot4(ld4(ap + k), ld4(bp + k));
-            acc = group_sum<G>(acc);
-            if (sub == 0 && ok) a.P[a.cmOut[ee]] = acc;
-        }
+    }
+}
+
+// ---- column-major residual slot, runtime K (multiple of 16): G = 4 lanes per entry
+__device__ __forceinline__ void residual_cm_generic(const SddmmArgs& a, const uint2 sl) {
+    constexpr u32 G = 4, NG = 16;
+    const u32 l = __lane_id(), sub = l % G, grp = l / G;
+    const u32 n = sl.y - sl.x;
+    const u32 share = (n + NG - 1) / NG;
+    const u32 gs = sl.x + min(grp * share, n), ge = sl.x + min(grp * share + share, n);
+    for (u32 e = gs; e < ge; ++e) {
+        const float* ap = a.A + static_cast<size_t>(a.cmRow[e]) * a.K;
+        const float* bp = a.B + static_cast<size_t>(a.cmCol[e]) * a.K;
+        float acc = 0.f;
+        for (u32 k = 4 * sub; k < a.K; k += 4 * G) acc += dot4(ld4(ap + k), ld4(bp + k));
+        acc = group_sum<G>(acc);
+        if (sub == 0) a.P[a.cmOut[e]] = acc;
     }
 }
 
@@ -198,15 +302,26 @@ __device__ __forceinline__ void residual_panel(const SddmmArgs& a, const uint4 i
     __syncthreads();
 }
 
-// full launch: blocks [0, nslots) residual slots, then dense items
+// full launch: dense tiles first (blocks [0, nd)), then residual slots from block ndpad =
+// roundup(nd, 8), so slot s runs on a block b with b % 8 == s % 8 (its column bucket's XCD)
 template <int KT, int G>
 __global__ __launch_bounds__(64) void k_sddmm_f32(SddmmArgs a) {
     const u32 b = blockIdx.x;
-    if (b < a.nslots) {
-        const uint2 sl = a.slots[b];
-        if (sl.x < sl.y) residual_cm<KT, G>(a, sl);
-    } else if (b - a.nslots < a.nd) {
-        dense_item<KT>(a, a.ditems[a.d0 + b - a.nslots]);
+    if (b < a.nd) {
+        dense_tile<KT>(a, a.d0 + b);
+        return;
+    }
+    const u32 ndpad = (a.nd + 7) & ~7u;
+    if (b < ndpad) return;
+    const u32 s = b - ndpad;
+    if (s < a.nslots) {
+        const uint2 sl = a.slots[s];
+        if (sl.x < sl.y) {
+            if constexpr (KT > 0)
+                residual_cm<KT>(a, sl);
+            else
+                residual_cm_generic(a, sl);
+        }
     }
 }
 
@@ -216,11 +331,13 @@ __global__ __launch_bounds__(64) void k_sddmm_panels_f32(SddmmArgs a) {
     extern __shared__ __attribute__((aligned(16))) float As[];
     const u32 b = blockIdx.x;
     if (b < a.nd) {
-        dense_item<KT>(a, a.ditems[a.d0 + b]);
+        dense_tile<KT>(a, a.d0 + b);
     } else if (b - a.nd < a.nr) {
         residual_panel<G>(a, a.ritems[a.r0 + b - a.nd], As);
     }
 }
+
+static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
 
 using KernelFn = void (*)(SddmmArgs);
 
@@ -266,7 +383,7 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
     a.A = static_cast<const float*>(dA);
     a.B = static_cast<const float*>(dB);
     a.P = dP;
-    a.ditems = p.denseItems.data();
+    a.tileRows = p.tileRows.data();
     a.rows = p.rows.data();
     a.R = p.R;
     a.N = p.N;
@@ -285,7 +402,7 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
 }
 
 int launch_full(SddmmArgs a, hipStream_t s) {
-    const u32 grid = a.nslots + a.nd;
+    const u32 grid = a.nslots ? ((a.nd + 7) & ~7u) + a.nslots : a.nd;
     if (grid == 0) return BSMR_OK;
     hipLaunchKernelGGL(pick_kernel<false>(a.K), dim3(grid), dim3(64), 0, s, a);
     BSMR_HIP(hipGetLastError());

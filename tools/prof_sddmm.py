@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Profiling driver: build the bench workload's plan once, then run the SDDMM kernel in its three
+forms (dense-tile items only, residual items only, fused) `iters` times each through
+bsmr_sddmm_profile, so rocprofv3 counter passes see only the launches of interest.
+
+    rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_sddmm --output-format csv \
+        -d gpurun_out/pmc_fetch -- python3 tools/prof_sddmm.py --iters 20
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sddmm-gpu_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--workload", default="nips_like")
+    args = ap.parse_args()
+    import torch
+
+    from bsmr import Plan, make_data, synth
+
+    M, N, rp, ci = getattr(synth, args.workload)()
+    K = args.K
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3)
+    dA = torch.from_numpy(make_data(M * K)).cuda()
+    dB = torch.from_numpy(make_data(N * K)).cuda()
+    dP = torch.zeros(len(ci), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s)
+    r = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=args.iters, stream=s)
+    torch.cuda.synchronize()
+    st = plan.stats()
+    print(json.dumps({"M": M, "N": N, "nnz": len(ci), "K": K, "timing_ms": r,
+                      "dense_items": st["dense_items"], "residual_slots_hint": st["residual_items"],
+                      "dense_tiles": st["num_dense_tiles"], "residual": st["num_residual"]}))
+
+
+if __name__ == "__main__":
+    main()
