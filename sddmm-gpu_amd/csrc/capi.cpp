@@ -1,6 +1,7 @@
 // capi.cpp — plan lifecycle, parity dumps, reorder statistics and sharding of the C ABI.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -54,6 +55,7 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     p.delta = o.delta;
     p.exact_all = o.exact_similarity;
     if (o.cluster_batch) p.cluster_batch = o.cluster_batch;
+    if (const char* ex = std::getenv("BSMR_EXEC")) p.use_rowblock = std::strcmp(ex, "rowblock") == 0;
     u64 free_mem = o.free_mem_bytes;
     if (free_mem == 0) {
         size_t fr = 0, tot = 0;

@@ -697,6 +697,36 @@ __global__ void k_cm_gather(const u32* __restrict__ order, const u32* __restrict
     if (i + 1 == n || skeys[i] / N != skeys[i + 1] / N) bucketCount[skeys[i] / N] = i + 1;
 }
 
+// Row-block layout: key = rowblock(q) * N + col (u64), q = reordered position of the entry's row.
+__global__ __launch_bounds__(256) void k_rb_keys(const u32* __restrict__ sdoff,
+                                                 const u32* __restrict__ sparseRel,
+                                                 const u32* __restrict__ sparseColIdx, u32 RB,
+                                                 u32 N, unsigned long long* __restrict__ keys,
+                                                 u32* __restrict__ vals, u32* __restrict__ qOf) {
+    const u32 p = blockIdx.x;
+    const u32 e0 = sdoff[p], e1 = sdoff[p + 1];
+    for (u32 e = e0 + threadIdx.x; e < e1; e += 256) {
+        const u32 q = p * 16 + sparseRel[e];
+        keys[e] = static_cast<unsigned long long>(q / RB) * N + sparseColIdx[e];
+        vals[e] = e;
+        qOf[e] = q;
+    }
+}
+
+__global__ void k_rb_gather(const u32* __restrict__ order, const u32* __restrict__ qOf,
+                            const u32* __restrict__ sparseColIdx,
+                            const u32* __restrict__ sparseValues, u32 n, u32 RB,
+                            u32* __restrict__ meta, u32* __restrict__ out, u32* __restrict__ rbEnd) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 e = order[i];
+    const u32 q = qOf[e];
+    meta[i] = ((q % RB) << 22) | sparseColIdx[e];
+    out[i] = sparseValues[e];
+    const u32 rb = q / RB;
+    if (i + 1 == n || qOf[order[i + 1]] / RB != rb) rbEnd[rb] = i + 1;
+}
+
 inline u32 grid_for(u64 n, u32 b) { return static_cast<u32>((n + b - 1) / b); }
 
 // exclusive scan of n values into out[0..n] (out[n] = total)
@@ -729,9 +759,21 @@ int read_one(const T* dptr, T& h, hipStream_t s) {
     return BSMR_OK;
 }
 
+int sort_pairs64(const unsigned long long* kin, unsigned long long* kout, const u32* vin, u32* vout,
+                 u32 n, int end_bit, DevBuf<uint8_t>& tmp, hipStream_t s) {
+    if (n == 0) return BSMR_OK;
+    size_t bytes = 0;
+    BSMR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout,
+                                                static_cast<int>(n), 0, end_bit, s));
+    if (bytes > tmp.size()) BSMR_CHECK(tmp.alloc(bytes));
+    BSMR_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.data(), bytes, kin, kout, vin, vout,
+                                                static_cast<int>(n), 0, end_bit, s));
+    return BSMR_OK;
+}
+
 int bits_for(u64 maxval) {
     int b = 1;
-    while (b < 32 && (1ull << b) <= maxval) ++b;
+    while (b < 64 && (1ull << b) <= maxval) ++b;
     return b;
 }
 
@@ -763,6 +805,87 @@ u32 kept_warp_mask(u32 B) {
     for (u32 stride = B / 64; stride >= 1; stride >>= 1)
         for (u32 w = 0; w < stride; ++w) reach[w] |= reach[w + stride];
     return reach[0];
+}
+
+// Rows per block for a K: largest power of two with RB * (K + 4) * 4 bytes <= 144 KiB of LDS.
+u32 rowblock_rows(u32 K) {
+    u32 rb = 1024;
+    while (rb > 16 && static_cast<u64>(rb) * (K + 4) * 4 > 144ull * 1024) rb >>= 1;
+    return rb;
+}
+
+int Plan::build_rowblock_layout(int slot, u32 K) const {
+    RowBlockLayout& L = rbl[slot];
+    hipStream_t s = stream;
+    const u32 RBr = rowblock_rows(K);
+    const u32 nRB = (R + RBr - 1) / RBr;
+    const u32 n = nres;
+    if (N > (1u << 22)) {
+        set_error("row-block layout needs N <= 2^22");
+        return BSMR_ERR_UNSUPPORTED;
+    }
+    BSMR_CHECK(L.meta.alloc(std::max<u32>(n, 1)));
+    BSMR_CHECK(L.out.alloc(std::max<u32>(n, 1)));
+    std::vector<u32> rbEnd(nRB, 0);
+    if (n) {
+        DevBuf<unsigned long long> keys, skeys;
+        DevBuf<u32> vals, order, qOf, dEnd;
+        BSMR_CHECK(keys.alloc(n));
+        BSMR_CHECK(skeys.alloc(n));
+        BSMR_CHECK(vals.alloc(n));
+        BSMR_CHECK(order.alloc(n));
+        BSMR_CHECK(qOf.alloc(n));
+        BSMR_CHECK(dEnd.alloc(nRB));
+        BSMR_HIP(hipMemsetAsync(dEnd.data(), 0, nRB * sizeof(u32), s));
+        hipLaunchKernelGGL(k_rb_keys, dim3(P), dim3(256), 0, s, sparseValueOffsets.data(),
+                           sparseRel.data(), sparseColIdx.data(), RBr, N, keys.data(), vals.data(),
+                           qOf.data());
+        BSMR_CHECK(sort_pairs64(keys.data(), skeys.data(), vals.data(), order.data(), n,
+                                bits_for(static_cast<u64>(nRB) * N), tmp, s));
+        hipLaunchKernelGGL(k_rb_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
+                           qOf.data(), sparseColIdx.data(), sparseValues.data(), n, RBr,
+                           L.meta.data(), L.out.data(), dEnd.data());
+        BSMR_HIP(hipGetLastError());
+        BSMR_HIP(hipMemcpyAsync(rbEnd.data(), dEnd.data(), nRB * sizeof(u32), hipMemcpyDeviceToHost, s));
+        BSMR_HIP(hipStreamSynchronize(s));
+        for (u32 b = 1; b < nRB; ++b) rbEnd[b] = std::max(rbEnd[b], rbEnd[b - 1]);
+    }
+    // balance: a dense tile ~ 16 residual entries; aim for ~2 items per CU, items of >= 1024 units
+    std::vector<u32> t0(nRB), t1(nRB), e0(nRB), e1(nRB);
+    double total = 0;
+    for (u32 b = 0; b < nRB; ++b) {
+        const u32 p0 = std::min(b * (RBr / 16), P), p1 = std::min((b + 1) * (RBr / 16), P);
+        t0[b] = h_blockOffsets[p0];
+        t1[b] = h_blockOffsets[p1];
+        e0[b] = b ? rbEnd[b - 1] : 0;
+        e1[b] = rbEnd[b];
+        total += 16.0 * (t1[b] - t0[b]) + (e1[b] - e0[b]);
+    }
+    const double target = std::max(total / 512.0, 1024.0);
+    std::vector<uint4> items;
+    std::vector<u32> ends;
+    for (u32 b = 0; b < nRB; ++b) {
+        const u32 nt = t1[b] - t0[b], ne = e1[b] - e0[b];
+        const double cost = 16.0 * nt + ne;
+        if (cost == 0) continue;
+        const u32 nch = std::max<u32>(1, static_cast<u32>(std::ceil(cost / target)));
+        for (u32 c = 0; c < nch; ++c) {
+            const u32 ta = t0[b] + static_cast<u32>(static_cast<u64>(nt) * c / nch);
+            const u32 tb = t0[b] + static_cast<u32>(static_cast<u64>(nt) * (c + 1) / nch);
+            const u32 ea = e0[b] + static_cast<u32>(static_cast<u64>(ne) * c / nch);
+            const u32 eb = e0[b] + static_cast<u32>(static_cast<u64>(ne) * (c + 1) / nch);
+            items.push_back(make_uint4(b, ta, tb, ea));
+            ends.push_back(eb);
+        }
+    }
+    L.nItems = static_cast<u32>(items.size());
+    BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
+    BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));
+    BSMR_HIP(hipStreamSynchronize(s));
+    L.RB = RBr;
+    L.nRB = nRB;
+    L.K = K;
+    return BSMR_OK;
 }
 
 int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
@@ -932,8 +1055,9 @@ int Plan::build_columns() {
             s));
         segments_ready = true;
     }
+    for (auto& L : rbl) L.K = 0;  // K-specific launch layouts depend on the column split
     // pass 1
-    const u32 thr = static_cast<u32>(std::ceil(delta * static_cast<float>(TILE)));  // colReordering.cu:246
+    const u32 thr =static_cast<u32>(std::ceil(delta * static_cast<float>(TILE)));  // colReordering.cu:246
     DevBuf<u32> phist, pnd, pns, psd;
     BSMR_CHECK(phist.alloc(16ull * P));
     BSMR_CHECK(pnd.alloc(P));

@@ -1,6 +1,7 @@
 // plan.hpp — the device-resident BSMR plan (reference BSMR + RPHM, include/BSMR.hpp:21-159).
 #pragma once
 
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -24,6 +25,9 @@ struct Plan {
     u32 bs = 16, nbpr = 1, B = 32, keptMask = 1;
     float alpha = 0.3f, delta = 0.3f;
     int exact_all = 0;
+    // launch layout: column-major residual slots (default) or row-block LDS items
+    // (BSMR_EXEC=rowblock at plan creation; experimental)
+    bool use_rowblock = false;
     u32 cluster_batch = 512;
 
     // input
@@ -56,7 +60,22 @@ struct Plan {
     DevBuf<uint2> cmSlots;
     u32 nSlots = 0;
 
-    DevBuf<uint8_t> tmp;  // scan/sort scratch
+    // Row-block launch layout for one K (built on first use): A rows of RB consecutive reordered
+    // positions staged in LDS; residual entries sorted by (row block, column) so one B read
+    // serves a column run; items {rb, t0, t1, e0} (+ e1 = next item's e0) balance tiles+entries.
+    struct RowBlockLayout {
+        u32 K = 0, RB = 0, nRB = 0, nItems = 0;
+        DevBuf<u32> meta;   // local row << 22 | column
+        DevBuf<u32> out;    // output index (CSR position)
+        DevBuf<uint4> items;
+        DevBuf<u32> itemEnd;
+    };
+    static constexpr int N_RB_LAYOUTS = 5;  // K = 32, 64, 128, 256, 512
+    mutable RowBlockLayout rbl[N_RB_LAYOUTS];
+    int build_rowblock_layout(int slot, u32 K) const;
+
+    mutable DevBuf<uint8_t> tmp;  // scan/sort scratch
+    mutable std::mutex layout_mu;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);
     int build_columns();

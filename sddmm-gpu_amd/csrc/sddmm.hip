@@ -337,6 +337,173 @@ __global__ __launch_bounds__(64) void k_sddmm_panels_f32(SddmmArgs a) {
     }
 }
 
+// ==========================================================================================
+// Row-block launch (default for K in {32, 64, 128, 256, 512}): one 1024-thread workgroup per
+// item {row block rb, tiles [t0, t1), residual entries [e0, e1)}. The A rows of the RB reordered
+// positions of rb are staged in LDS once (up to ~135 KB of the CU's 160 KB); dense tiles take
+// their MFMA A operand and residual entries their A pieces from LDS, so the only gathered operand
+// is B, read once per column run (entries are sorted by (row block, column)).
+// ==========================================================================================
+struct RbArgs {
+    const float* A;
+    const float* B;
+    float* P;
+    const u32* rows;
+    u32 R, N, RB;
+    const uint4* items;
+    const u32* itemEnd;
+    const u32* meta;  // local row << 22 | column
+    const u32* out;
+    const uint4* tilePanel;  // dense work items: .x = panel of the tile
+    const u32* denseCols;
+    const u32* blockValues;
+    u32 mode;  // 1 = dense tiles, 2 = residual, 3 = both
+};
+
+template <int KT>
+__device__ __forceinline__ void dense_tile_lds(const RbArgs& a, const u32 tile, const float* As,
+                                               const u32 q0) {
+    constexpr u32 LD = KT + 4;
+    const u32 l = __lane_id(), rr = l & 15, g = l >> 4;
+    const u32 p = a.tilePanel[tile].x;
+    const u32 c = a.denseCols[tile * 16 + rr];
+    const u32* bvals = a.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
+    u32 idx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) idx[r] = bvals[16 * r];
+    const bool cvalid = c < a.N;
+    const float* arow = As + (p * 16 - q0 + rr) * LD + 4 * g;
+    const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * KT + 4 * g;
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+    constexpr int NK = KT / 16;
+    constexpr int CH = NK < 8 ? NK : 8;
+#pragma unroll
+    for (int k0 = 0; k0 < NK; k0 += CH) {
+        f32x4 bv[CH];
+#pragma unroll
+        for (int kk = 0; kk < CH; ++kk)
+            bv[kk] = cvalid ? ld4(bcol + 16 * (k0 + kk)) : f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < CH; ++kk) {
+            const f32x4 av = *reinterpret_cast<const f32x4*>(arow + 16 * (k0 + kk));
+            f32x4& acc = (kk & 1) ? acc1 : acc0;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[kk].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[kk].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[kk].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[kk].w, acc, 0, 0, 0);
+        }
+    }
+    const f32x4 acc = acc0 + acc1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (idx[r] != NULLV) a.P[idx[r]] = acc[r];
+}
+
+// residual entries [e0, e1) of the item; 64 row-groups (16 waves x 4) take contiguous shares
+template <int KT>
+__device__ __forceinline__ void residual_rb(const RbArgs& a, const u32 e0, const u32 e1,
+                                            const float* As, const u32 w) {
+    constexpr int W = KT >= 64 ? 4 : KT / 16;
+    constexpr int NF = KT / (16 * W);
+    constexpr int U = NF >= 8 ? 1 : 8 / NF;
+    constexpr u32 LD = KT + 4;
+    typedef typename vec<W>::t vt;
+    const u32 l = __lane_id(), sub = l & 15, grp = w * 4 + (l >> 4);
+    const u32 n = e1 - e0;
+    const u32 share = (n + 63) / 64;
+    const u32 gs = e0 + min(grp * share, n), ge = e0 + min(grp * share + share, n);
+    u32 curc = NULLV;
+    vt bcur[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) bcur[f] = vt{};
+    for (u32 base = gs; base < ge; base += 16) {
+        const u32 e = base + sub;
+        const bool okm = e < ge;
+        const u32 mmeta = okm ? a.meta[e] : NULLV;
+        const u32 mout = okm ? a.out[e] : 0u;
+        const u32 nb = min(16u, ge - base);
+#pragma unroll
+        for (int i0 = 0; i0 < 16; i0 += U) {
+            if (static_cast<u32>(i0) >= nb) break;
+            vt av[U][NF], bv[U][NF];
+            u32 cc[U], oo[U];
+            bool ok[U], chg[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                u32 m;
+                switch (i0 + u) {
+#define BSMR_B(I)                   \
+    case I:                         \
+        m = row_bcast<I>(mmeta);    \
+        oo[u] = row_bcast<I>(mout); \
+        break;
+                    BSMR_B(0) BSMR_B(1) BSMR_B(2) BSMR_B(3) BSMR_B(4) BSMR_B(5) BSMR_B(6) BSMR_B(7)
+                    BSMR_B(8) BSMR_B(9) BSMR_B(10) BSMR_B(11) BSMR_B(12) BSMR_B(13) BSMR_B(14)
+                    BSMR_B(15)
+#undef BSMR_B
+                    default:
+                        m = NULLV;
+                        oo[u] = 0;
+                }
+                ok[u] = static_cast<u32>(i0 + u) < nb;
+                cc[u] = m & 0x3FFFFFu;
+                const u32 lr = ok[u] ? (m >> 22) : 0u;
+                const u32 prev = u ? cc[u - 1] : curc;
+                chg[u] = ok[u] && cc[u] != prev;
+                const float* ap = As + lr * LD + W * sub;
+#pragma unroll
+                for (int f = 0; f < NF; ++f) av[u][f] = *reinterpret_cast<const vt*>(ap + 16 * W * f);
+                if (chg[u]) {
+                    const float* bp = a.B + static_cast<size_t>(cc[u]) * KT + W * sub;
+#pragma unroll
+                    for (int f = 0; f < NF; ++f)
+                        bv[u][f] = *reinterpret_cast<const vt*>(bp + 16 * W * f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!chg[u]) {
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) bv[u][f] = u ? bv[u - 1][f] : bcur[f];
+                }
+                float acc = 0.f;
+#pragma unroll
+                for (int f = 0; f < NF; ++f) acc += vdot<W>(av[u][f], bv[u][f]);
+                acc = row_sum16(acc);
+                if (sub == 0 && ok[u]) a.P[oo[u]] = acc;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) {
+                    curc = cc[u];
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) bcur[f] = bv[u][f];
+                }
+        }
+    }
+}
+
+template <int KT>
+__global__ __launch_bounds__(1024) void k_sddmm_rb(RbArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float As[];
+    constexpr u32 LD = KT + 4, K4 = KT / 4;
+    const uint4 it = a.items[blockIdx.x];
+    const u32 q0 = it.x * a.RB;
+    const u32 tid = threadIdx.x;
+    for (u32 x = tid; x < a.RB * K4; x += 1024) {
+        const u32 lr = x / K4, k4 = x - lr * K4;
+        const u32 q = q0 + lr;
+        const f32x4 v = q < a.R ? ld4(a.A + static_cast<size_t>(a.rows[q]) * KT + 4 * k4)
+                                : f32x4{0, 0, 0, 0};
+        *reinterpret_cast<f32x4*>(As + lr * LD + 4 * k4) = v;
+    }
+    __syncthreads();
+    const u32 w = tid >> 6;
+    if (a.mode & 1)
+        for (u32 t = it.y + w; t < it.z; t += 16) dense_tile_lds<KT>(a, t, As, q0);
+    if (a.mode & 2) residual_rb<KT>(a, it.w, a.itemEnd[blockIdx.x], As, w);
+}
+
 static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
 
 using KernelFn = void (*)(SddmmArgs);
@@ -401,6 +568,60 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
     return a;
 }
 
+// K -> row-block layout slot (-1: use the column-major path)
+int rb_slot(const Plan& p, u32 K) {
+    if (p.N > (1u << 22) || !p.use_rowblock) return -1;
+    switch (K) {
+        case 32: return 0;
+        case 64: return 1;
+        case 128: return 2;
+        case 256: return 3;
+        case 512: return 4;
+        default: return -1;
+    }
+}
+
+int ensure_rb_layout(const Plan& p, int slot, u32 K) {
+    std::lock_guard<std::mutex> g(p.layout_mu);
+    if (p.rbl[slot].K == K) return BSMR_OK;
+    return p.build_rowblock_layout(slot, K);
+}
+
+// mode: 1 = dense tiles only, 2 = residual only, 3 = both (profiling splits)
+int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP, u32 mode,
+              hipStream_t s) {
+    const Plan::RowBlockLayout& L = p.rbl[slot];
+    if (L.nItems == 0) return BSMR_OK;
+    RbArgs a{};
+    a.A = static_cast<const float*>(dA);
+    a.B = static_cast<const float*>(dB);
+    a.P = dP;
+    a.rows = p.rows.data();
+    a.R = p.R;
+    a.N = p.N;
+    a.RB = L.RB;
+    a.items = L.items.data();
+    a.itemEnd = L.itemEnd.data();
+    a.meta = L.meta.data();
+    a.out = L.out.data();
+    a.tilePanel = p.denseItems.data();
+    a.denseCols = p.denseCols.data();
+    a.blockValues = p.blockValues.data();
+    a.mode = mode;
+    const size_t lds = static_cast<size_t>(L.RB) * (L.K + 4) * sizeof(float);
+    void (*fn)(RbArgs) = nullptr;
+    switch (L.K) {
+        case 32: fn = k_sddmm_rb<32>; break;
+        case 64: fn = k_sddmm_rb<64>; break;
+        case 128: fn = k_sddmm_rb<128>; break;
+        case 256: fn = k_sddmm_rb<256>; break;
+        default: fn = k_sddmm_rb<512>; break;
+    }
+    hipLaunchKernelGGL(fn, dim3(L.nItems), dim3(1024), lds, s, a);
+    BSMR_HIP(hipGetLastError());
+    return BSMR_OK;
+}
+
 int launch_full(SddmmArgs a, hipStream_t s) {
     const u32 grid = a.nslots ? ((a.nd + 7) & ~7u) + a.nslots : a.nd;
     if (grid == 0) return BSMR_OK;
@@ -431,6 +652,11 @@ extern "C" int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB,
     }
     const Plan& p = plan->p;
     BSMR_CHECK(validate(dA, dB, K, dtype, dP));
+    const int slot = rb_slot(p, K);
+    if (slot >= 0) {
+        BSMR_CHECK(ensure_rb_layout(p, slot, K));
+        return launch_rb(p, slot, dA, dB, dP, 3, static_cast<hipStream_t>(stream));
+    }
     SddmmArgs a = make_args(p, dA, dB, K, dP);
     a.nd = p.nDenseItems;
     a.nslots = p.nSlots;
@@ -485,6 +711,8 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipEvent_t ev[4];
     for (auto& e : ev) BSMR_HIP(hipEventCreate(&e));
+    const int slot = rb_slot(p, K);
+    if (slot >= 0) BSMR_CHECK(ensure_rb_layout(p, slot, K));
     SddmmArgs full = make_args(p, dA, dB, K, dP);
     full.nd = p.nDenseItems;
     full.nslots = p.nSlots;
@@ -492,12 +720,16 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     dense.nslots = 0;
     SddmmArgs res = full;
     res.nd = 0;
+    auto run = [&](u32 mode) -> int {
+        if (slot >= 0) return launch_rb(p, slot, dA, dB, dP, mode, s);
+        return launch_full(mode == 1 ? dense : mode == 2 ? res : full, s);
+    };
     BSMR_HIP(hipEventRecord(ev[0], s));
-    for (int i = 0; i < iters; ++i) BSMR_CHECK(launch_full(dense, s));
+    for (int i = 0; i < iters; ++i) BSMR_CHECK(run(1));
     BSMR_HIP(hipEventRecord(ev[1], s));
-    for (int i = 0; i < iters; ++i) BSMR_CHECK(launch_full(res, s));
+    for (int i = 0; i < iters; ++i) BSMR_CHECK(run(2));
     BSMR_HIP(hipEventRecord(ev[2], s));
-    for (int i = 0; i < iters; ++i) BSMR_CHECK(launch_full(full, s));
+    for (int i = 0; i < iters; ++i) BSMR_CHECK(run(3));
     BSMR_HIP(hipEventRecord(ev[3], s));
     BSMR_HIP(hipEventSynchronize(ev[3]));
     float t0 = 0, t1 = 0, t2 = 0;
@@ -505,7 +737,7 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     BSMR_HIP(hipEventElapsedTime(&t1, ev[1], ev[2]));
     BSMR_HIP(hipEventElapsedTime(&t2, ev[2], ev[3]));
     if (ms_dense) *ms_dense = p.nDenseItems ? t0 / iters : 0.f;
-    if (ms_residual) *ms_residual = p.nSlots ? t1 / iters : 0.f;
+    if (ms_residual) *ms_residual = p.nres ? t1 / iters : 0.f;
     if (ms_total) *ms_total = t2 / iters;
     for (auto& e : ev) (void)hipEventDestroy(e);
     return BSMR_OK;
