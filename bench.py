@@ -93,14 +93,14 @@ def main():
 
     from bsmr import Plan, make_data, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from bsmr import dist as D
+
+    rank, world, local = D.env_rank_world()
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        D.init("nccl")  # RCCL over xGMI
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -125,7 +125,7 @@ def main():
     if dist is not None:
         torch.cuda.synchronize()
         tb = time.perf_counter()
-        dist.broadcast(dB, src=0)  # B broadcast once over RCCL/xGMI
+        D.broadcast_(dB, 0)  # B broadcast once over RCCL/xGMI
         torch.cuda.synchronize()
         bcast_ms = (time.perf_counter() - tb) * 1e3
     dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
@@ -148,9 +148,7 @@ def main():
         dist.barrier()
     ms = e0.elapsed_time(e1)
     if dist is not None:
-        t = torch.tensor([ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms = float(t.item())
+        ms = D.max_over_ranks(ms, dev)  # whole-job time = slowest rank
     ms_per_step = ms / args.steps
 
     # per-part timing of the same kernel (dense-tile items only / residual items only)

@@ -14,6 +14,11 @@ constexpr u32 RES_PER_ITEM = 256;   // residual entries per panel-major wave ite
 constexpr u32 CM_PER_ITEM = 64;     // residual entries per column-major wave item (full launch)
 constexpr u32 XCD_BUCKETS = 8;      // MI355X XCDs: column bucket c % 8 -> blocks b with b % 8
 
+struct Plan;
+// fp16/bf16 SDDMM launch (sddmm_half.hip); mode: 1 dense tiles, 2 residual, 3 both
+int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
+                u32 mode, hipStream_t s);
+
 u32 block_size_for(u32 M, u32 N, u64 free_mem);
 u32 cluster_block_dim(u32 nbpr);
 u32 kept_warp_mask(u32 B);

@@ -538,8 +538,8 @@ int validate(const void* dA, const void* dB, u32 K, int dtype, const float* dP) 
         set_error("bsmr_sddmm: K must be a positive multiple of 16");
         return BSMR_ERR_UNSUPPORTED;
     }
-    if (dtype != BSMR_F32) {
-        set_error("bsmr_sddmm: this build supports fp32 A/B only");
+    if (dtype != BSMR_F32 && dtype != BSMR_F16 && dtype != BSMR_BF16) {
+        set_error("bsmr_sddmm: dtype must be BSMR_F32, BSMR_F16 or BSMR_BF16");
         return BSMR_ERR_UNSUPPORTED;
     }
     return BSMR_OK;
@@ -652,6 +652,7 @@ extern "C" int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB,
     }
     const Plan& p = plan->p;
     BSMR_CHECK(validate(dA, dB, K, dtype, dP));
+    if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, 3, static_cast<hipStream_t>(stream));
     const int slot = rb_slot(p, K);
     if (slot >= 0) {
         BSMR_CHECK(ensure_rb_layout(p, slot, K));
@@ -672,6 +673,10 @@ extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const vo
     }
     const Plan& p = plan->p;
     BSMR_CHECK(validate(dA, dB, K, dtype, dP));
+    if (dtype != BSMR_F32) {
+        set_error("bsmr_sddmm_panels: panel ranges support fp32 A/B only");
+        return BSMR_ERR_UNSUPPORTED;
+    }
     if (p0 > p1 || p1 > p.P) {
         set_error("bsmr_sddmm_panels: bad panel range");
         return BSMR_ERR_INVALID;
@@ -721,6 +726,7 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     SddmmArgs res = full;
     res.nd = 0;
     auto run = [&](u32 mode) -> int {
+        if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, mode, s);
         if (slot >= 0) return launch_rb(p, slot, dA, dB, dP, mode, s);
         return launch_full(mode == 1 ? dense : mode == 2 ? res : full, s);
     };

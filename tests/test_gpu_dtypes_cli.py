@@ -1,0 +1,131 @@
+"""GPU: fp16/bf16 inputs (configs C3/C5) and the BSMR-sddmm drop-in binary."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from bsmr import BF16, F16, Plan, make_data, synth
+from gpu_util import torch_cuda
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "sddmm-gpu_amd", "bin", "BSMR-sddmm")
+FREE = 288 * 1024 ** 3
+
+
+def to_bf16_bits(x):
+    b = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((b + 0x7FFF + ((b >> 16) & 1)) >> 16).astype(np.uint16)
+    return r, (r.astype(np.uint32) << 16).view(np.float32)
+
+
+def to_f16_bits(x):
+    h = np.ascontiguousarray(x, np.float32).astype(np.float16)
+    return h.view(np.uint16), h.astype(np.float32)
+
+
+def run_half(plan, Ab, Bb, K, nnz, dtype):
+    torch = torch_cuda()
+    dA = torch.from_numpy(Ab.view(np.int16)).cuda()
+    dB = torch.from_numpy(Bb.view(np.int16)).cuda()
+    dP = torch.full((nnz,), float("nan"), dtype=torch.float32, device="cuda")
+    plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+               stream=torch.cuda.current_stream().cuda_stream, dtype=dtype)
+    torch.cuda.synchronize()
+    return dP.cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype", [F16, BF16])
+@pytest.mark.parametrize("K", [32, 96, 256, 512])
+@pytest.mark.parametrize("case", ["blocky", "zipf"])
+def test_half_inputs_checkdata(dtype, K, case):
+    if case == "blocky":
+        M, N, rp, ci = synth.block_mask(512, 16, 0.1, seed=7)
+    else:
+        M, N, rp, ci = synth.random_rows(400, 3000, 50, seed=8, zipf=1.1)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    A = make_data(M * K)
+    B = make_data(N * K)
+    conv = to_bf16_bits if dtype == BF16 else to_f16_bits
+    Ab, Ar = conv(A)
+    Bb, Br = conv(B)
+    P = run_half(plan, Ab, Bb, K, len(ci), dtype)
+    assert np.isfinite(P).all()
+    # oracle in fp32 on the same rounded values: half x half products are exact in fp32
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, Ar, Br)
+    assert O.check_data(ref, P) == 0
+
+
+def test_dlmc_like_bf16_k512():
+    M, N, rp, ci = synth.uniform_mask(2048, 0.1, seed=7)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    K = 512
+    Ab, Ar = to_bf16_bits(make_data(M * K))
+    Bb, Br = to_bf16_bits(make_data(N * K))
+    P = run_half(plan, Ab, Bb, K, len(ci), BF16)
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, Ar, Br)
+    assert O.check_data(ref, P) == 0
+
+
+def _log_fields(text):
+    return dict(re.findall(r"\[([A-Za-z_]+)\s*: ([^\]]*)\]", text))
+
+
+def test_cli_default_run_log(tmp_path):
+    M, N, rp, ci = synth.random_rows(600, 2000, 40, seed=9, zipf=1.05)
+    path = str(tmp_path / "s.mtx")
+    synth.write_mtx(path, M, N, rp, ci)
+    r = subprocess.run([BIN, "-f", path, "-k", "64", "-a", "0.3", "-d", "0.3"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert f"sparseMatrix::CSR initialize from file : {path}" in r.stdout
+    f = _log_fields(r.stdout)
+    assert f["K"] == "64" and f["M"] == str(M) and f["NNZ"] == str(len(ci))
+    assert f["matrixA storageOrder"] == "row_major" and f["matrixB storageOrder"] == "col_major"
+    assert f["bsmr_alpha"] == "0.30" and f["bsmr_delta"] == "0.30"
+    # reorder statistics equal the oracle's
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    rows, ncl, _ = O.row_reorder(c, np.float32(0.3), O.block_size(M, N, FREE))
+    s = O.Plan(c, rows, ncl, np.float32(0.3)).stats()
+    assert int(f["bsmr_numClusters"]) == ncl
+    assert int(f["NumRowPanel"]) == s["numRowPanels"]
+    assert int(f["bsmr_numDenseBlock"]) == s["numDenseBlock"]
+    assert int(f["bsmr_numSparseData"]) == s["numSparseData"]
+    assert float(f["bsmr_gflops"]) > 0
+    # the reference analysis script's parser (analyze_results.cpp getValue) finds the key
+    assert re.search(r"\[bsmr_gflops : [0-9.]+\]", r.stdout)
+
+
+def test_cli_positional_and_failure(tmp_path):
+    M, N, rp, ci = synth.random_rows(100, 300, 10, seed=10)
+    path = str(tmp_path / "p.mtx")
+    synth.write_mtx(path, M, N, rp, ci)
+    r = subprocess.run([BIN, path, "32"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "[K : 32]" in r.stdout
+    bad = str(tmp_path / "bad.mtx")
+    open(bad, "w").write("%x\n2 2 2\n1 1 1\n1 1 1\n")
+    r = subprocess.run([BIN, "-f", bad], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 255
+    assert "Error, matrix S initialize failed." in r.stderr
+
+
+def test_cli_test_mode_writes_reference_log_files(tmp_path):
+    M, N, rp, ci = synth.random_rows(200, 800, 20, seed=11)
+    path = str(tmp_path / "t.mtx")
+    synth.write_mtx(path, M, N, rp, ci)
+    logdir = str(tmp_path) + "/"
+    r = subprocess.run([BIN, "-f", path, "-t", "1", "-l", logdir], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stderr
+    names = sorted(os.listdir(tmp_path))
+    logs = [n for n in names if n.startswith("BSMR_k_")]
+    assert len(logs) == 5 * 7 * 4
+    assert "BSMR_k_128_a_0.3_d_0.3.log" in logs and "BSMR_k_32_a_0.1_d_0.log" in logs
+    assert "BSMR_k_256_a_0.9_d_1.1.log" in logs
+    text = open(os.path.join(tmp_path, "BSMR_k_128_a_0.3_d_0.3.log")).read()
+    assert text.startswith("\n---New data---\n")
+    assert _log_fields(text)["bsmr_delta"] == "0.30"
