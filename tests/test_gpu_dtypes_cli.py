@@ -72,7 +72,7 @@ def test_dlmc_like_bf16_k512():
 
 
 def _log_fields(text):
-    return dict(re.findall(r"\[([A-Za-z_]+)\s*: ([^\]]*)\]", text))
+    return dict(re.findall(r"\[([A-Za-z_][A-Za-z_ ]*?)\s*: ([^\]]*)\]", text))
 
 
 def test_cli_default_run_log(tmp_path):
