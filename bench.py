@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """bench.py — SDDMM GFLOP/s (2*nnz*K) of the BSMR engine on MI355X, reference headline metric.
 
-Step = one SDDMM pass (the fused dense-tile MFMA + residual launch) over the plan of the C2
-workload of BASELINE.json: nips-like 1,500 x 12,419 pattern (~746k nnz; the real nips.mtx is a
-missing blob of the reference), K = 128, fp32 A/B, alpha = delta = 0.3. Reordering happens once
-before timing and is reported separately (the reference's GFLOP/s excludes it too,
-Logger.hpp:178-180). Inputs are resident in HBM when the timed region starts.
+Default (the driver's line): step = one SDDMM pass (one launch: dense-tile MFMA + residual) over
+the plan of the C2 workload of BASELINE.json: nips-like 1,500 x 12,419 pattern with 746,316 nnz
+(the real nips.mtx is a missing blob of the reference), K = 128, fp32 A/B, alpha = delta = 0.3.
+Reordering runs once before timing and is reported separately (the reference's GFLOP/s excludes it
+too, Logger.hpp:178-180). Inputs are resident in HBM when the timed region starts.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak scaling.
-Rank r owns row block r of an N-times taller pattern (each block the C2 pattern), builds that
-block's plan, and holds its own A rows; B is generated on rank 0 and broadcast once over RCCL
-(xGMI) before timing. There is no collective in the data path; value = all ranks' flops / the
-slowest rank's time.
+Rank r owns row block r of an N-times taller pattern (each block the chosen workload's pattern),
+builds that block's plan and holds its A rows; B is generated on rank 0 and broadcast once over
+RCCL (xGMI) before timing. No collective in the data path; value = all ranks' flops / the slowest
+rank's time.
+
+Other BASELINE.json configs (extra measurements, not the driver's line): --config C3 (cop20k-like,
+fp16, K=256), C4 (reddit-like power-law graph, fp32, K=128; --scale shrinks it), C5 (DLMC-like
+2048^2 90 % sparse mask, bf16, K=512; --mask uniform|block).
 """
 import argparse
 import json
@@ -32,13 +36,33 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--K", type=int, default=None)
     ap.add_argument("--alpha", type=float, default=0.3)
     ap.add_argument("--delta", type=float, default=0.3)
+    ap.add_argument("--scale", type=float, default=1.0, help="C4 size factor")
+    ap.add_argument("--mask", default="uniform", choices=["uniform", "block"], help="C5 mask")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
-                    help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic")
+                    help="PMC summary with hbm_bytes_per_launch for roofline.traffic")
     return ap.parse_args()
+
+
+def workload(args):
+    from bsmr import F16, F32, BF16, synth
+
+    if args.config == "C2":
+        M, N, rp, ci = synth.nips_like()
+        return (M, N, rp, ci), args.K or 128, F32, (
+            "C2: nips_like 1500x12419, 746,316 nnz (Zipf 1.1 columns, seed 20250801), fp32 A/B")
+    if args.config == "C3":
+        return synth.cop20k_like(), args.K or 256, F16, (
+            "C3: cop20k_A_like 121192^2 FEM band+random (seed 20250802), fp16 A/B, fp32 accumulate")
+    if args.config == "C4":
+        return synth.reddit_like(args.scale), args.K or 128, F32, (
+            f"C4: reddit_like Chung-Lu power law x{args.scale} (seed 20250803), fp32 A/B")
+    return synth.dlmc_like(args.mask), args.K or 512, BF16, (
+        f"C5: dlmc_like 2048^2 90% sparse {args.mask} mask (seed 7), bf16 A/B, fp32 accumulate")
 
 
 def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
@@ -50,21 +74,28 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     c = O.CSR.from_arrays(M, N, rp, ci)
-    P = np.empty(len(ci), np.float32)
     lib = O.lib()
     Af = np.ascontiguousarray(A, np.float32)
     Bf = np.ascontiguousarray(B, np.float32)
-    lib.orc_sddmm_cpu(c.h, K, Af, Bf, P, threads)  # warm-up
+    # bounded sample: whole rows from the start, about 2 GFLOP of work per run
+    budget = 2e9
+    row_end, acc = M, 0.0
+    for r in range(M):
+        acc += 2.0 * (int(rp[r + 1]) - int(rp[r])) * K
+        if acc >= budget:
+            row_end = r + 1
+            break
+    nnz_s = int(rp[row_end])
+    P = np.empty(len(ci), np.float32)
+    lib.orc_sddmm_cpu_rows(c.h, K, Af, Bf, P, 0, row_end, threads)  # warm-up
     times = []
     t_end = time.perf_counter() + 20.0
     while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 50):
         t0 = time.perf_counter()
-        lib.orc_sddmm_cpu(c.h, K, Af, Bf, P, threads)
+        lib.orc_sddmm_cpu_rows(c.h, K, Af, Bf, P, 0, row_end, threads)
         times.append(time.perf_counter() - t0)
-        if len(times) >= 5 and time.perf_counter() > t_end:
-            break
     med = statistics.median(times)
-    nerr = O.check_data(P, P_gpu)
+    nerr = O.check_data(P[:nnz_s], P_gpu[:nnz_s])
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -74,13 +105,14 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
                     break
     except OSError:
         pass
+    full = "full workload" if row_end == M else f"rows [0, {row_end}) of {M}"
     return {
-        "value": round(2.0 * len(ci) * K / med / 1e9, 3),
+        "value": round(2.0 * nnz_s * K / med / 1e9, 3),
         "unit": "GFLOP/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"full C2 workload (nnz={len(ci)}, K={K}), median of {len(times)} runs "
-                  f"after 1 warm-up, OpenMP over rows; cpu: {model}",
+        "sample": f"{full} (nnz={nnz_s}, K={K}), median of {len(times)} runs after 1 warm-up, "
+                  f"OpenMP over rows (oracle/oracle.cpp orc_sddmm_cpu_rows); cpu: {model}",
         "ms": round(med * 1e3, 3),
         "checkData_errors_vs_gpu": nerr,
     }
@@ -91,8 +123,7 @@ def main():
     import numpy as np
     import torch
 
-    from bsmr import Plan, make_data, synth
-
+    from bsmr import F32, Plan, make_data
     from bsmr import dist as D
 
     rank, world, local = D.env_rank_world()
@@ -105,22 +136,22 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    K = args.K
-    M, N, rp, ci = synth.nips_like()
+    (M, N, rp, ci), K, dtype, desc = workload(args)
     nnz = len(ci)
     t0 = time.perf_counter()
     plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, device=dev.index)
     plan_s = time.perf_counter() - t0
     st = plan.stats()
 
+    tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
     A = make_data(M * K)  # this rank's A rows (Matrix<float>(M,K,row_major).makeData)
-    dA = torch.from_numpy(A).to(dev)
+    dA = torch.from_numpy(A).to(dev).to(tdt)
     if rank == 0:
         B = make_data(N * K)
-        dB = torch.from_numpy(B).to(dev)
+        dB = torch.from_numpy(B).to(dev).to(tdt)
     else:
         B = None
-        dB = torch.empty(N * K, dtype=torch.float32, device=dev)
+        dB = torch.empty(N * K, dtype=tdt, device=dev)
     bcast_ms = 0.0
     if dist is not None:
         torch.cuda.synchronize()
@@ -132,8 +163,11 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
+    def step():
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp, dtype=dtype)
+
     for _ in range(args.warmup):
-        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp)
+        step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -141,7 +175,7 @@ def main():
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(args.steps):
-        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp)
+        step()
     e1.record(stream)
     torch.cuda.synchronize()
     if dist is not None:
@@ -151,13 +185,15 @@ def main():
         ms = D.max_over_ranks(ms, dev)  # whole-job time = slowest rank
     ms_per_step = ms / args.steps
 
-    # per-part timing of the same kernel (dense-tile items only / residual items only)
-    prof = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=20, stream=sp)
+    # the same kernel split into its dense-tile-only and residual-only launches
+    prof = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=20, stream=sp,
+                        dtype=dtype)
     P_gpu = dP.cpu().numpy()
 
+    s = 4 if dtype == F32 else 2
     flops_rank = 2.0 * nnz * K
     value = flops_rank * world / (ms_per_step * 1e-3) / 1e9
-    bytes_alg = 4.0 * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
+    bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
     achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
@@ -168,6 +204,7 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
+    kern = {0: "k_sddmm_f32", 1: "k_sddmm_half<f16>", 2: "k_sddmm_half<bf16>"}[dtype]
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -179,16 +216,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": {0: "f32", 1: "f16", 2: "bf16"}[dtype],
         "data": "synthetic",
         "config": {
-            "workload": "C2: nips_like 1500x12419 (Zipf 1.1 columns, seed 20250801), K=128, "
-                        "fp32 A/B, BSMR alpha=0.3 delta=0.3, 1 plan per rank (row block)",
+            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}, "
+                               "one plan per rank (row block)",
             "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
             "parallelism": f"row-panel blocks x{world}, B broadcast (RCCL)",
             "num_clusters": st["num_clusters"], "dense_tiles": st["num_dense_tiles"],
-            "residual_nnz": st["num_residual"], "dense_items": st["dense_items"],
-            "residual_items": st["residual_items"],
+            "residual_nnz": st["num_residual"],
             "plan_build_s": round(plan_s, 3), "row_reorder_ms": round(st["row_reorder_ms"], 3),
             "col_reorder_ms": round(st["col_reorder_ms"], 3), "b_broadcast_ms": round(bcast_ms, 3),
         },
@@ -199,13 +235,18 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "k_sddmm_f32<128,16> (fused dense MFMA + residual)",
+            "kernel": f"{kern}<{K}> (one launch: dense-tile MFMA + residual)",
             "bytes_alg_per_launch": bytes_alg,
         },
         "kernels_ms": {k: round(v, 5) for k, v in prof.items()},
     }
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(M, N, rp, ci, K, A, B, P_gpu)
+        if dtype == F32:
+            Ar, Br = A, B
+        else:  # the oracle runs in fp32 on the same rounded half values
+            Ar = dA.float().cpu().numpy()
+            Br = dB.float().cpu().numpy()
+        out["cpu_baseline"] = cpu_baseline(M, N, rp, ci, K, Ar, Br, P_gpu)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

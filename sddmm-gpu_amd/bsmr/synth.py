@@ -132,6 +132,52 @@ def banded_fem_like(n, nnz_per_row, seed, band=64):
     return _csr_from_coo(n, n, key // n, key % n)
 
 
+def cop20k_like(seed=20250802):
+    """C3 stand-in: 121,192 x 121,192 FEM-like pattern, ~21.7 nnz/row (2.62M)."""
+    return banded_fem_like(121192, 22, seed, band=48)
+
+
+def chung_lu(n, nnz_target, seed, exponent=2.2, chunk=20_000_000):
+    """Symmetric power-law graph (Chung-Lu): endpoints drawn with probability proportional to
+    w_i = (i+1)^(-1/(exponent-1)); both directions stored, duplicates and self loops dropped."""
+    rng = np.random.default_rng(seed)
+    w = (np.arange(1, n + 1, dtype=np.float64)) ** (-1.0 / (exponent - 1.0))
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    perm = rng.permutation(n)
+    keys = []
+    drawn = 0
+    need = int(nnz_target * 0.53)  # undirected draws; duplicates are removed below
+    while drawn < need:
+        m = min(chunk, need - drawn)
+        i = perm[np.searchsorted(cdf, rng.random(m))]
+        j = perm[np.searchsorted(cdf, rng.random(m))]
+        keep = i != j
+        i, j = i[keep], j[keep]
+        keys.append(i.astype(np.int64) * n + j)
+        keys.append(j.astype(np.int64) * n + i)
+        drawn += m
+    key = np.unique(np.concatenate(keys))
+    rows = key // n
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(rowptr, rows + 1, 1)
+    return n, n, np.cumsum(rowptr).astype(np.uint32), (key % n).astype(np.uint32)
+
+
+def reddit_like(scale=1.0, seed=20250803):
+    """C4 stand-in: 232,965-node power-law graph, ~232M stored entries at scale 1 (BASELINE.json
+    quotes ~232M nnz; the public Reddit graph has 114,615,892 edges). scale < 1 shrinks both."""
+    n = max(1024, int(232965 * scale))
+    return chung_lu(n, int(232_000_000 * scale * scale), seed)
+
+
+def dlmc_like(kind="uniform", seed=7):
+    """C5 stand-in: 2,048 x 2,048 transformer mask at 90 % sparsity, uniform or 16x16 blocks."""
+    if kind == "uniform":
+        return uniform_mask(2048, 0.1, seed)
+    return block_mask(2048, 16, 0.1, seed)
+
+
 def block_mask(n, block, density, seed):
     """DLMC-like 2-D mask: 16x16 (block) structured at the given block density."""
     rng = np.random.default_rng(seed)
