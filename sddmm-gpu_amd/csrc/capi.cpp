@@ -56,6 +56,7 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     p.exact_all = o.exact_similarity;
     if (o.cluster_batch) p.cluster_batch = o.cluster_batch;
     if (const char* ex = std::getenv("BSMR_EXEC")) p.use_rowblock = std::strcmp(ex, "rowblock") == 0;
+    if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
     u64 free_mem = o.free_mem_bytes;
     if (free_mem == 0) {
         size_t fr = 0, tot = 0;

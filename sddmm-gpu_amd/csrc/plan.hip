@@ -1137,12 +1137,16 @@ int Plan::build_columns() {
             begins[b] = b ? ends[b - 1] : 0;
             rmax = std::max(rmax, (ends[b] - begins[b] + CM_PER_ITEM - 1) / CM_PER_ITEM);
         }
+        // the launch runs 4 waves (slots) per workgroup and deals workgroups round-robin over
+        // the 8 XCDs: slot s lives in workgroup s / 4, on XCD (s / 4) % 8 = its bucket
+        rmax = (rmax + 3) & ~3u;
         nSlots = rmax * XCD_BUCKETS;
         std::vector<uint2> slots(std::max<u32>(nSlots, 1), make_uint2(0, 0));
         for (u32 b = 0; b < XCD_BUCKETS; ++b)
             for (u32 j = 0; j < rmax; ++j) {
                 const u32 e0 = std::min(begins[b] + j * CM_PER_ITEM, ends[b]);
-                slots[j * XCD_BUCKETS + b] = make_uint2(e0, std::min(e0 + CM_PER_ITEM, ends[b]));
+                const u32 s = ((j / 4) * XCD_BUCKETS + b) * 4 + (j % 4);
+                slots[s] = make_uint2(e0, std::min(e0 + CM_PER_ITEM, ends[b]));
             }
         BSMR_CHECK(cmSlots.upload(slots.data(), slots.size(), s));
         BSMR_HIP(hipStreamSynchronize(s));  // `slots` is pageable host memory

@@ -33,6 +33,7 @@ struct Plan {
     // launch layout: column-major residual slots (default) or row-block LDS items
     // (BSMR_EXEC=rowblock at plan creation; experimental)
     bool use_rowblock = false;
+    u32 diag = 0;  // BSMR_DIAG profiling ablations (wrong results; never set in normal use)
     u32 cluster_batch = 512;
 
     // input

@@ -51,6 +51,7 @@ struct SddmmArgs {
     const u32* sparseValues;
     const u32* sparseRel;
     const u32* sparseCol;
+    u32 diag;  // profiling ablations (BSMR_DIAG); always 0 in normal use
 };
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -77,9 +78,10 @@ __device__ __forceinline__ void dense_tile(const SddmmArgs& a, const u32 tile) {
     const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * K + 4 * g;
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};  // two chains halve the MFMA dependency
     if constexpr (KT > 0) {
-        // chunks of at most 8 k-steps (128 k): 16 float4 = 64 VGPRs of operands in flight
+        // chunks of at most 4 k-steps (64 k): 8 float4 = 32 VGPRs of operands in flight, so the
+        // kernel fits 64 VGPRs (8 waves per SIMD)
         constexpr int NK = KT / 16;
-        constexpr int CH = NK < 8 ? NK : 8;
+        constexpr int CH = NK < 4 ? NK : 4;
 #pragma unroll
         for (int k0 = 0; k0 < NK; k0 += CH) {
             f32x4 av[CH], bv[CH];
@@ -110,7 +112,7 @@ __device__ __forceinline__ void dense_tile(const SddmmArgs& a, const u32 tile) {
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-        if (idx[r] != NULLV) a.P[idx[r]] = acc[r];
+        if (idx[r] != NULLV && (!(a.diag & 1) || acc[r] == -1234.5f)) a.P[idx[r]] = acc[r];
 }
 
 template <int G>
@@ -175,7 +177,7 @@ template <int KT>
 __device__ __forceinline__ void residual_cm(const SddmmArgs& a, const uint2 sl) {
     constexpr int W = KT >= 64 ? 4 : KT / 16;
     constexpr int NF = KT / (16 * W);
-    constexpr int U = NF >= 8 ? 1 : 8 / NF;
+    constexpr int U = NF >= 4 ? 1 : 4 / NF;  // <= 64 VGPRs: 8 waves per SIMD
     typedef typename vec<W>::t vt;
     const u32 l = __lane_id(), sub = l & 15, grp = l >> 4;
     const u32 n = sl.y - sl.x;
@@ -222,12 +224,15 @@ __device__ __forceinline__ void residual_cm(const SddmmArgs& a, const uint2 sl) 
                 ok[u] = static_cast<u32>(i0 + u) < nb;
                 const u32 prev = u ? cc[u - 1] : curc;
                 chg[u] = ok[u] && cc[u] != prev;
-                const float* ap = a.A + static_cast<size_t>(ok[u] ? r : 0) * KT + W * sub;
+                // a.diag (profiling ablations only; 0 in every real launch): 2 = A row 0, 4 = B col 0
+                const u32 ar = (a.diag & 2) ? 0u : (ok[u] ? r : 0u);
+                const float* ap = a.A + static_cast<size_t>(ar) * KT + W * sub;
 #pragma unroll
                 for (int f = 0; f < NF; ++f)
                     av[u][f] = *reinterpret_cast<const vt*>(ap + 16 * W * f);
                 if (chg[u]) {
-                    const float* bp = a.B + static_cast<size_t>(cc[u]) * KT + W * sub;
+                    const u32 bc = (a.diag & 4) ? 0u : cc[u];
+                    const float* bp = a.B + static_cast<size_t>(bc) * KT + W * sub;
 #pragma unroll
                     for (int f = 0; f < NF; ++f)
                         bv[u][f] = *reinterpret_cast<const vt*>(bp + 16 * W * f);
@@ -243,7 +248,8 @@ __device__ __forceinline__ void residual_cm(const SddmmArgs& a, const uint2 sl) 
 #pragma unroll
                 for (int f = 0; f < NF; ++f) acc += vdot<W>(av[u][f], bv[u][f]);
                 acc = row_sum16(acc);
-                if (sub == 0 && ok[u]) a.P[oo[u]] = acc;
+                // diag 1: store only an impossible value (keeps the math, drops the P scatter)
+                if (sub == 0 && ok[u] && (!(a.diag & 1) || acc == -1234.5f)) a.P[oo[u]] = acc;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -302,16 +308,18 @@ __device__ __forceinline__ void residual_panel(const SddmmArgs& a, const uint4 i
     __syncthreads();
 }
 
-// full launch: dense tiles first (blocks [0, nd)), then residual slots from block ndpad =
-// roundup(nd, 8), so slot s runs on a block b with b % 8 == s % 8 (its column bucket's XCD)
+// full launch: 256-thread workgroups of four independent waves, one work item per wave (no LDS,
+// no barriers); <= 64 VGPRs so 8 waves per SIMD (32 per CU) are resident. Items [0, nd) are dense
+// tiles, residual slots start at item ndpad = roundup(nd, 32), so slot s sits in block
+// (ndpad + s) / 4 whose XCD (block % 8) is the slot's column bucket (slot layout in plan.hip).
 template <int KT, int G>
-__global__ __launch_bounds__(64) void k_sddmm_f32(SddmmArgs a) {
-    const u32 b = blockIdx.x;
+__global__ __launch_bounds__(256, (KT >= 256 ? 4 : 8)) void k_sddmm_f32(SddmmArgs a) {
+    const u32 b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b < a.nd) {
         dense_tile<KT>(a, a.d0 + b);
         return;
     }
-    const u32 ndpad = (a.nd + 7) & ~7u;
+    const u32 ndpad = (a.nd + 31) & ~31u;
     if (b < ndpad) return;
     const u32 s = b - ndpad;
     if (s < a.nslots) {
@@ -565,6 +573,7 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
     a.sparseValues = p.sparseValues.data();
     a.sparseRel = p.sparseRel.data();
     a.sparseCol = p.sparseColIdx.data();
+    a.diag = p.diag;
     return a;
 }
 
@@ -623,9 +632,9 @@ int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP
 }
 
 int launch_full(SddmmArgs a, hipStream_t s) {
-    const u32 grid = a.nslots ? ((a.nd + 7) & ~7u) + a.nslots : a.nd;
-    if (grid == 0) return BSMR_OK;
-    hipLaunchKernelGGL(pick_kernel<false>(a.K), dim3(grid), dim3(64), 0, s, a);
+    const u32 items = a.nslots ? ((a.nd + 31) & ~31u) + a.nslots : a.nd;
+    if (items == 0) return BSMR_OK;
+    hipLaunchKernelGGL(pick_kernel<false>(a.K), dim3((items + 3) / 4), dim3(256), 0, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }
