@@ -71,7 +71,14 @@ typedef struct {
     int device;               /* HIP device ordinal */
     uint32_t cluster_batch;   /* clusters per persistent launch; 0 = default */
     int exact_similarity;     /* !=0: evaluate every similarity with the exact fp32 tree */
+    int layout;               /* SDDMM launch layout: BSMR_LAYOUT_AUTO / _ROWBLOCK / _COLMAJOR */
+    uint32_t lds_budget_kb;   /* LDS per row-block workgroup, 16..160 KiB; 0 = default (144) */
 } bsmr_plan_options;
+
+/* AUTO = ROWBLOCK: A rows staged in LDS per row block, K in {64, 128, 256, 512}, column-major
+ * residual slots for other K. COLMAJOR: column-major slots for every K. Results are identical
+ * up to fp32 summation order (checkData tolerance). */
+enum { BSMR_LAYOUT_AUTO = 0, BSMR_LAYOUT_ROWBLOCK = 1, BSMR_LAYOUT_COLMAJOR = 2 };
 
 void bsmr_plan_options_default(bsmr_plan_options* o);
 

@@ -39,7 +39,11 @@ class BsmrError(RuntimeError):
 class PlanOptions(C.Structure):
     _fields_ = [("alpha", C.c_float), ("delta", C.c_float), ("free_mem_bytes", C.c_uint64),
                 ("device", C.c_int), ("cluster_batch", C.c_uint32),
-                ("exact_similarity", C.c_int)]
+                ("exact_similarity", C.c_int), ("layout", C.c_int),
+                ("lds_budget_kb", C.c_uint32)]
+
+
+LAYOUTS = {"auto": 0, "rowblock": 1, "colmajor": 2}
 
 
 class PlanStats(C.Structure):
@@ -196,7 +200,7 @@ class Plan:
     """Device-resident BSMR plan (reordered rows, dense 16x16 tiles, residual lists)."""
 
     def __init__(self, M, N, rowptr, colidx, alpha=0.3, delta=0.3, free_mem_bytes=0, device=0,
-                 cluster_batch=0, exact_similarity=False):
+                 cluster_batch=0, exact_similarity=False, layout="auto", lds_budget_kb=0):
         rowptr = np.ascontiguousarray(rowptr, np.uint32)
         colidx = np.ascontiguousarray(colidx, np.uint32)
         o = PlanOptions()
@@ -207,6 +211,8 @@ class Plan:
         o.device = int(device)
         o.cluster_batch = int(cluster_batch)
         o.exact_similarity = 1 if exact_similarity else 0
+        o.layout = LAYOUTS[layout]
+        o.lds_budget_kb = int(lds_budget_kb)
         self.M, self.N, self.nnz = int(M), int(N), int(len(colidx))
         h = C.c_void_p()
         _check(lib().bsmr_plan_create(rowptr, colidx, M, N, len(colidx), C.byref(o), C.byref(h)),

@@ -18,6 +18,8 @@ extern "C" void bsmr_plan_options_default(bsmr_plan_options* o) {
     o->device = 0;
     o->cluster_batch = 0;
     o->exact_similarity = 0;
+    o->layout = BSMR_LAYOUT_AUTO;
+    o->lds_budget_kb = 0;
 }
 
 extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M,
@@ -55,7 +57,13 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     p.delta = o.delta;
     p.exact_all = o.exact_similarity;
     if (o.cluster_batch) p.cluster_batch = o.cluster_batch;
-    if (const char* ex = std::getenv("BSMR_EXEC")) p.use_rowblock = std::strcmp(ex, "rowblock") == 0;
+    if (o.layout < BSMR_LAYOUT_AUTO || o.layout > BSMR_LAYOUT_COLMAJOR ||
+        (o.lds_budget_kb && (o.lds_budget_kb < 16 || o.lds_budget_kb > 160))) {
+        set_error("bsmr_plan_create: bad layout or lds_budget_kb");
+        return fail(BSMR_ERR_INVALID);
+    }
+    p.use_rowblock = o.layout != BSMR_LAYOUT_COLMAJOR;
+    if (o.lds_budget_kb) p.rb_lds_kb = o.lds_budget_kb;
     if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
     u64 free_mem = o.free_mem_bytes;
     if (free_mem == 0) {

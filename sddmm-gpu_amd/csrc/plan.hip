@@ -807,26 +807,59 @@ u32 kept_warp_mask(u32 B) {
     return reach[0];
 }
 
-// Rows per block for a K: largest power of two with RB * (K + 4) * 4 bytes <= 144 KiB of LDS.
-u32 rowblock_rows(u32 K) {
-    u32 rb = 1024;
-    while (rb > 16 && static_cast<u64>(rb) * (K + 4) * 4 > 144ull * 1024) rb >>= 1;
-    return rb;
+// Rows per row block for a K: a multiple of 16 with RB * K * 4 bytes within the LDS budget, at
+// most 1024 (10-bit local row in the entry metadata) and no more than the matrix needs.
+u32 rowblock_rows(u32 K, u32 lds_kb, u32 R) {
+    u32 rb = static_cast<u32>(static_cast<u64>(lds_kb) * 1024 / (4ull * K) / 16 * 16);
+    rb = std::min<u32>(std::max<u32>(rb, 16), 1024);
+    return std::min<u32>(rb, std::max<u32>((R + 15) / 16 * 16, 16));
 }
+
+namespace {
+// split q chunks over segments by cost (largest remainder); every non-empty segment gets >= 1
+std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
+    const size_t n = cost.size();
+    std::vector<u32> out(n, 0);
+    double tot = 0;
+    for (double c : cost) tot += c;
+    if (tot <= 0) return out;
+    std::vector<std::pair<double, size_t>> frac;
+    u32 used = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (cost[i] <= 0) continue;
+        const double ideal = q * cost[i] / tot;
+        out[i] = std::max<u32>(1, static_cast<u32>(std::floor(ideal)));
+        used += out[i];
+        frac.push_back({ideal - std::floor(ideal), i});
+    }
+    std::stable_sort(frac.begin(), frac.end(),
+                     [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (size_t k = 0; used < q && k < frac.size(); ++k, ++used) ++out[frac[k].second];
+    return out;
+}
+}  // namespace
 
 int Plan::build_rowblock_layout(int slot, u32 K) const {
     RowBlockLayout& L = rbl[slot];
+    L.K = 0;
     hipStream_t s = stream;
-    const u32 RBr = rowblock_rows(K);
-    const u32 nRB = (R + RBr - 1) / RBr;
-    const u32 n = nres;
     if (N > (1u << 22)) {
         set_error("row-block layout needs N <= 2^22");
         return BSMR_ERR_UNSUPPORTED;
     }
+    const u32 RBr = rowblock_rows(K, rb_lds_kb, R);
+    const u32 nRB = (R + RBr - 1) / RBr;
+    const size_t lds = static_cast<size_t>(RBr) * K * sizeof(float);
+    const u32 NT = lds > 80 * 1024 ? 1024 : 512;
+    const u32 wgPerCU = std::max<u32>(1, std::min<u32>(static_cast<u32>(160 * 1024 / lds), 2048 / NT));
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256;
+    const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
+    const u32 n = nres;
     BSMR_CHECK(L.meta.alloc(std::max<u32>(n, 1)));
     BSMR_CHECK(L.out.alloc(std::max<u32>(n, 1)));
-    std::vector<u32> rbEnd(nRB, 0);
+    std::vector<u32> rbEnd(nRB, 0), hmeta(n);
     if (n) {
         DevBuf<unsigned long long> keys, skeys;
         DevBuf<u32> vals, order, qOf, dEnd;
@@ -847,42 +880,113 @@ int Plan::build_rowblock_layout(int slot, u32 K) const {
                            L.meta.data(), L.out.data(), dEnd.data());
         BSMR_HIP(hipGetLastError());
         BSMR_HIP(hipMemcpyAsync(rbEnd.data(), dEnd.data(), nRB * sizeof(u32), hipMemcpyDeviceToHost, s));
+        BSMR_HIP(hipMemcpyAsync(hmeta.data(), L.meta.data(), n * sizeof(u32), hipMemcpyDeviceToHost, s));
         BSMR_HIP(hipStreamSynchronize(s));
         for (u32 b = 1; b < nRB; ++b) rbEnd[b] = std::max(rbEnd[b], rbEnd[b - 1]);
     }
-    // balance: a dense tile ~ 16 residual entries; aim for ~2 items per CU, items of >= 1024 units
-    std::vector<u32> t0(nRB), t1(nRB), e0(nRB), e1(nRB);
-    double total = 0;
-    for (u32 b = 0; b < nRB; ++b) {
-        const u32 p0 = std::min(b * (RBr / 16), P), p1 = std::min((b + 1) * (RBr / 16), P);
-        t0[b] = h_blockOffsets[p0];
-        t1[b] = h_blockOffsets[p1];
-        e0[b] = b ? rbEnd[b - 1] : 0;
-        e1[b] = rbEnd[b];
-        total += 16.0 * (t1[b] - t0[b]) + (e1[b] - e0[b]);
+    // column cuts: XCD_BUCKETS ranges of (nearly) equal residual count
+    constexpr u32 CM = (1u << 22) - 1;
+    std::vector<u32> cuts(XCD_BUCKETS + 1, N);
+    cuts[0] = 0;
+    {
+        std::vector<u32> cnt(N + 1, 0);
+        for (u32 i = 0; i < n; ++i) ++cnt[hmeta[i] & CM];
+        u64 run = 0;
+        u32 x = 1;
+        for (u32 c = 0; c < N && x < XCD_BUCKETS; ++c) {
+            while (x < XCD_BUCKETS && run >= static_cast<u64>(n) * x / XCD_BUCKETS) cuts[x++] = c;
+            run += cnt[c];
+        }
+        for (; x < XCD_BUCKETS; ++x) cuts[x] = N;
     }
-    const double target = std::max(total / 512.0, 1024.0);
-    std::vector<uint4> items;
-    std::vector<u32> ends;
+    // segments (rb, bucket): entries of rb in the bucket's column range + 1/8 of rb's tiles
+    const u32 nseg = nRB * XCD_BUCKETS;
+    std::vector<u32> se0(nseg), se1(nseg), st0(nseg), st1(nseg);
+    std::vector<double> cost(nseg);
     for (u32 b = 0; b < nRB; ++b) {
-        const u32 nt = t1[b] - t0[b], ne = e1[b] - e0[b];
-        const double cost = 16.0 * nt + ne;
-        if (cost == 0) continue;
-        const u32 nch = std::max<u32>(1, static_cast<u32>(std::ceil(cost / target)));
-        for (u32 c = 0; c < nch; ++c) {
-            const u32 ta = t0[b] + static_cast<u32>(static_cast<u64>(nt) * c / nch);
-            const u32 tb = t0[b] + static_cast<u32>(static_cast<u64>(nt) * (c + 1) / nch);
-            const u32 ea = e0[b] + static_cast<u32>(static_cast<u64>(ne) * c / nch);
-            const u32 eb = e0[b] + static_cast<u32>(static_cast<u64>(ne) * (c + 1) / nch);
-            items.push_back(make_uint4(b, ta, tb, ea));
-            ends.push_back(eb);
+        const u32 eb0 = b ? rbEnd[b - 1] : 0, eb1 = rbEnd[b];
+        const u32 p0 = std::min(b * (RBr / 16), P), p1 = std::min((b + 1) * (RBr / 16), P);
+        const u32 t0 = h_blockOffsets[p0], nt = h_blockOffsets[p1] - t0;
+        for (u32 x = 0; x < XCD_BUCKETS; ++x) {
+            const u32 i = b * XCD_BUCKETS + x;
+            auto lb = [&](u32 col) {
+                return static_cast<u32>(std::lower_bound(hmeta.begin() + eb0, hmeta.begin() + eb1, col,
+                                                         [](u32 m, u32 c) { return (m & CM) < c; }) -
+                                        hmeta.begin());
+            };
+            se0[i] = x ? lb(cuts[x]) : eb0;
+            se1[i] = x + 1 < XCD_BUCKETS ? lb(cuts[x + 1]) : eb1;
+            st0[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * x / XCD_BUCKETS);
+            st1[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * (x + 1) / XCD_BUCKETS);
+            cost[i] = (se1[i] - se0[i]) + 16.0 * (st1[i] - st0[i]);
         }
     }
+    // chunks per bucket: one round of workgroup slots unless items would drop below ~512 units
+    std::vector<std::vector<uint4>> lists(XCD_BUCKETS);
+    std::vector<std::vector<u32>> lends(XCD_BUCKETS);
+    const double minItem = 512.0;
+    for (u32 x = 0; x < XCD_BUCKETS; ++x) {
+        std::vector<double> cx(nRB);
+        double tx = 0;
+        for (u32 b = 0; b < nRB; ++b) tx += (cx[b] = cost[b * XCD_BUCKETS + x]);
+        if (tx <= 0) continue;
+        const u32 rounds = std::max<u32>(1, static_cast<u32>(std::ceil(tx / (perBucket * 65536.0))));
+        const u32 q = std::max<u32>(1, std::min<u32>(perBucket * rounds, static_cast<u32>(tx / minItem)));
+        const std::vector<u32> nch = apportion(cx, q);
+        for (u32 b = 0; b < nRB; ++b) {
+            const u32 i = b * XCD_BUCKETS + x;
+            const u32 ne = se1[i] - se0[i], nt = st1[i] - st0[i];
+            for (u32 c = 0; c < nch[b]; ++c) {
+                const u32 ea = se0[i] + static_cast<u32>(static_cast<u64>(ne) * c / nch[b]);
+                const u32 eb = se0[i] + static_cast<u32>(static_cast<u64>(ne) * (c + 1) / nch[b]);
+                const u32 ta = st0[i] + static_cast<u32>(static_cast<u64>(nt) * c / nch[b]);
+                const u32 tb = st0[i] + static_cast<u32>(static_cast<u64>(nt) * (c + 1) / nch[b]);
+                if (ea == eb && ta == tb) continue;
+                lists[x].push_back(make_uint4(b, ta, tb, ea));
+                lends[x].push_back(eb);
+            }
+        }
+    }
+    size_t nmax = 0;
+    for (const auto& l : lists) nmax = std::max(nmax, l.size());
+    std::vector<uint4> items(nmax * XCD_BUCKETS, make_uint4(0, 0, 0, 0));
+    std::vector<u32> ends(nmax * XCD_BUCKETS, 0);
+    for (u32 x = 0; x < XCD_BUCKETS; ++x)
+        for (size_t j = 0; j < lists[x].size(); ++j) {
+            items[j * XCD_BUCKETS + x] = lists[x][j];
+            ends[j * XCD_BUCKETS + x] = lends[x][j];
+        }
+    // column-run pieces: each item's entries [e0, e1) cut at column changes and every
+    // RB_PIECE_MAX entries; piece {first entry, column | (length - 1) << 22}, longest first so
+    // the 16 row-groups of a wave get pieces of similar length
+    std::vector<uint2> pieces;
+    pieces.reserve(n / 4 + items.size());
+    std::vector<uint2> mine;
+    for (size_t i = 0; i < items.size(); ++i) {
+        const u32 ea = items[i].w, eb = ends[i];
+        mine.clear();
+        for (u32 e = ea; e < eb;) {
+            const u32 col = hmeta[e] & CM;
+            u32 f = e + 1;
+            while (f < eb && f - e < RB_PIECE_MAX && (hmeta[f] & CM) == col) ++f;
+            mine.push_back(make_uint2(e, col | ((f - e - 1) << 22)));
+            e = f;
+        }
+        std::stable_sort(mine.begin(), mine.end(),
+                         [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
+        items[i].w = static_cast<u32>(pieces.size());
+        pieces.insert(pieces.end(), mine.begin(), mine.end());
+        ends[i] = static_cast<u32>(pieces.size());
+    }
     L.nItems = static_cast<u32>(items.size());
+    L.nPieces = static_cast<u32>(pieces.size());
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
     BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));
+    BSMR_CHECK(L.pieces.upload(pieces.data(), std::max<size_t>(pieces.size(), 1), s));
     BSMR_HIP(hipStreamSynchronize(s));
     L.RB = RBr;
+    L.NT = NT;
+    L.lds = lds;
     L.nRB = nRB;
     L.K = K;
     return BSMR_OK;

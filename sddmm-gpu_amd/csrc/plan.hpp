@@ -12,7 +12,8 @@ namespace bsmr {
 constexpr u32 TILES_PER_ITEM = 1;   // dense tiles per wave item
 constexpr u32 RES_PER_ITEM = 256;   // residual entries per panel-major wave item (panel ranges)
 constexpr u32 CM_PER_ITEM = 64;     // residual entries per column-major wave item (full launch)
-constexpr u32 XCD_BUCKETS = 8;      // MI355X XCDs: column bucket c % 8 -> blocks b with b % 8
+constexpr u32 RB_PIECE_MAX = 16;    // entries per column-run piece (row-block layout)
+constexpr u32 XCD_BUCKETS = 8;      // MI355X XCDs: column bucket -> workgroups b with b % 8
 
 struct Plan;
 // fp16/bf16 SDDMM launch (sddmm_half.hip); mode: 1 dense tiles, 2 residual, 3 both
@@ -30,9 +31,10 @@ struct Plan {
     u32 bs = 16, nbpr = 1, B = 32, keptMask = 1;
     float alpha = 0.3f, delta = 0.3f;
     int exact_all = 0;
-    // launch layout: column-major residual slots (default) or row-block LDS items
-    // (BSMR_EXEC=rowblock at plan creation; experimental)
-    bool use_rowblock = false;
+    // launch layout (bsmr_plan_options.layout): row-block LDS items for K in {64, 128, 256, 512}
+    // unless BSMR_LAYOUT_COLMAJOR; the column-major residual slots for every other K
+    bool use_rowblock = true;
+    u32 rb_lds_kb = 144;  // LDS budget of a row-block workgroup (bsmr_plan_options.lds_budget_kb)
     u32 diag = 0;  // BSMR_DIAG profiling ablations (wrong results; never set in normal use)
     u32 cluster_batch = 512;
 
@@ -66,21 +68,38 @@ struct Plan {
     DevBuf<uint2> cmSlots;
     u32 nSlots = 0;
 
-    // Row-block launch layout for one K (built on first use): A rows of RB consecutive reordered
-    // positions staged in LDS; residual entries sorted by (row block, column) so one B read
-    // serves a column run; items {rb, t0, t1, e0} (+ e1 = next item's e0) balance tiles+entries.
+    // Row-block launch layout for one K (built on first use): the A rows of RB consecutive
+    // reordered positions are staged in LDS once per workgroup; residual entries are sorted by
+    // (row block, column) so one B read serves a column run. The columns are cut into 8 ranges of
+    // equal residual count, one per XCD; item i {rb, t0, t1, e0} (+ itemEnd[i]) holds a chunk of
+    // row block rb's entries in column range i % 8 (so its B columns sit in that XCD's L2) and a
+    // share of rb's dense tiles; about one item per workgroup slot of the chip.
+    // Residual entries of an item are cut into column-run pieces of <= RB_PIECE_MAX entries; the
+    // 4-lane row-groups of a workgroup take one piece each per phase, so every group loads its B
+    // column in the same (full-width) instruction. items[i].w / itemEnd[i] delimit its pieces.
     struct RowBlockLayout {
-        u32 K = 0, RB = 0, nRB = 0, nItems = 0;
+        u32 K = 0, RB = 0, NT = 1024, nRB = 0, nItems = 0, nPieces = 0;
+        size_t lds = 0;
         DevBuf<u32> meta;   // local row << 22 | column
         DevBuf<u32> out;    // output index (CSR position)
         DevBuf<uint4> items;
         DevBuf<u32> itemEnd;
+        DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}
     };
-    static constexpr int N_RB_LAYOUTS = 5;  // K = 32, 64, 128, 256, 512
+    static constexpr int N_RB_LAYOUTS = 2;  // K = 64, 128
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
     int build_rowblock_layout(int slot, u32 K) const;
 
     mutable DevBuf<uint8_t> tmp;  // scan/sort scratch
+    // BSMR_DIAG & 32 debug timeline (4 u64 per wave of the last launch)
+    mutable DevBuf<unsigned long long> trace;
+    mutable size_t traceN = 0;
+    int prepare_trace(size_t waves, hipStream_t s) const {
+        if (trace.size() < waves * 4) BSMR_CHECK(trace.alloc(waves * 4));
+        BSMR_HIP(hipMemsetAsync(trace.data(), 0, waves * 4 * sizeof(unsigned long long), s));
+        traceN = waves;
+        return BSMR_OK;
+    }
     mutable std::mutex layout_mu;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);

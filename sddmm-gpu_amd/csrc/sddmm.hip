@@ -52,7 +52,25 @@ struct SddmmArgs {
     const u32* sparseRel;
     const u32* sparseCol;
     u32 diag;  // profiling ablations (BSMR_DIAG); always 0 in normal use
+    unsigned long long* trace;  // BSMR_DIAG & 32: per-wave {start, mid, end, hw id}; else null
 };
+
+// debug timeline (BSMR_DIAG & 32 only): wave start / mid / end in s_memrealtime ticks (100 MHz)
+// and the wave's XCC id << 32 | HW_ID register
+__device__ __forceinline__ unsigned long long rtime(const void* on) {
+    return on ? __builtin_amdgcn_s_memrealtime() : 0ull;
+}
+__device__ __forceinline__ void trace_wave(unsigned long long* tr, u32 slot, unsigned long long t0,
+                                           unsigned long long tm, unsigned long long td = 0) {
+    if (tr && __lane_id() == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const u32 xcc = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID, 32 bits
+        tr[4ull * slot + 0] = t0;
+        tr[4ull * slot + 1] = tm;
+        tr[4ull * slot + 2] = t1;
+        tr[4ull * slot + 3] = (static_cast<unsigned long long>(xcc) << 60) | (td ? td : tm);
+    }
+}
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ float dot4(f32x4 a, f32x4 b) {
@@ -314,9 +332,11 @@ __device__ __forceinline__ void residual_panel(const SddmmArgs& a, const uint4 i
 // (ndpad + s) / 4 whose XCD (block % 8) is the slot's column bucket (slot layout in plan.hip).
 template <int KT, int G>
 __global__ __launch_bounds__(256, (KT >= 256 ? 4 : 8)) void k_sddmm_f32(SddmmArgs a) {
+    const unsigned long long t0 = rtime(a.trace);
     const u32 b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b < a.nd) {
         dense_tile<KT>(a, a.d0 + b);
+        trace_wave(a.trace, b, t0, t0);
         return;
     }
     const u32 ndpad = (a.nd + 31) & ~31u;
@@ -331,6 +351,7 @@ __global__ __launch_bounds__(256, (KT >= 256 ? 4 : 8)) void k_sddmm_f32(SddmmArg
                 residual_cm_generic(a, sl);
         }
     }
+    trace_wave(a.trace, b, t0, t0);
 }
 
 // panel-range launch: dense items of the range, then its panel-major residual items
@@ -346,11 +367,23 @@ __global__ __launch_bounds__(64) void k_sddmm_panels_f32(SddmmArgs a) {
 }
 
 // ==========================================================================================
-// Row-block launch (default for K in {32, 64, 128, 256, 512}): one 1024-thread workgroup per
-// item {row block rb, tiles [t0, t1), residual entries [e0, e1)}. The A rows of the RB reordered
-// positions of rb are staged in LDS once (up to ~135 KB of the CU's 160 KB); dense tiles take
-// their MFMA A operand and residual entries their A pieces from LDS, so the only gathered operand
-// is B, read once per column run (entries are sorted by (row block, column)).
+// Row-block launch (K = 64, 128): one workgroup per item {row block rb, tiles [t0, t1), residual
+// entries [e0, e1)} (layout: Plan::build_rowblock_layout). The A rows of the RB reordered
+// positions of rb are staged in LDS once (<= 144 KiB); dense tiles take their MFMA A operand and
+// residual entries their A pieces from LDS, so the only gathered operand is B, read once per
+// column run (entries are sorted by (row block, column)), from the L2 of the XCD that owns the
+// item's column range.
+//
+// Residual entries: G = 4 lanes per entry (16 row-groups per wave), so the per-entry bookkeeping
+// (metadata broadcast, addresses, column-change test, store) is shared by 16 entries per wave
+// instruction; each lane owns NC = K/16 chunks (16 B) 4t + s of the row, multiplies them with
+// packed FMAs and the quad reduces with two DPP adds.
+// LDS image: row lr at lr * K floats (unpadded); chunk c of row lr sits at
+// (c & ~3) | ((c & 3) ^ (lr & 3)). Lane (row-group j, sub s) visits its chunks in the rotated
+// order t = (f + j) mod NC, so in every ds_read_b128 lane group ({0-3,12-15,20-27},
+// {4-11,16-19,28-31}, +32 = row-groups {0,3,5,6}, {1,2,4,7}, ...) the four row-groups read four
+// different 64-byte quads: conflict-free for any rows (the XOR only permutes inside a quad).
+// Dense tiles read chunk 16w + 4g + j of the 16 tile rows: the XOR spreads rows 0-3 (2-way).
 // ==========================================================================================
 struct RbArgs {
     const float* A;
@@ -358,158 +391,233 @@ struct RbArgs {
     float* P;
     const u32* rows;
     u32 R, N, RB;
-    const uint4* items;
-    const u32* itemEnd;
-    const u32* meta;  // local row << 22 | column
+    const uint4* items;     // {row block, tile begin, tile end, piece begin}
+    const u32* itemEnd;     // piece end
+    const uint2* pieces;    // {first entry, column | (length - 1) << 22}
+    const u32* meta;        // local row << 22 | column
     const u32* out;
     const uint4* tilePanel;  // dense work items: .x = panel of the tile
     const u32* denseCols;
     const u32* blockValues;
     u32 mode;  // 1 = dense tiles, 2 = residual, 3 = both
+    unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
+    u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
 };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u32 lds_chunk(u32 lr, u32 c) { return (c & ~3u) | ((c & 3u) ^ (lr & 3u)); }
+
+// value of lane I of the quad in every lane of the quad
+template <int I>
+__device__ __forceinline__ u32 quad_bcast(u32 v) {
+    return static_cast<u32>(
+        __builtin_amdgcn_update_dpp(0, static_cast<int>(v), I * 0x55, 0xF, 0xF, false));
+}
+
+// dense tile on the LDS image: load() gathers the tile's metadata and B operand (no LDS, so a
+// wave can issue it before the staging barrier), run() reads the A rows from LDS, runs the MFMAs
+// and scatters the 256 outputs
 template <int KT>
-__device__ __forceinline__ void dense_tile_lds(const RbArgs& a, const u32 tile, const float* As,
-                                               const u32 q0) {
-    constexpr u32 LD = KT + 4;
-    const u32 l = __lane_id(), rr = l & 15, g = l >> 4;
-    const u32 p = a.tilePanel[tile].x;
-    const u32 c = a.denseCols[tile * 16 + rr];
-    const u32* bvals = a.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
-    u32 idx[4];
+struct DenseTileLds {
+    static constexpr int NK = KT / 16;  // k-steps; step kk = 4w + j covers chunks 16w + 4g + j
+    u32 lr, idx[4];
+    __device__ __forceinline__ static u32 chunk(int kk, u32 g) {
+        return 16 * (kk >> 2) + 4 * g + (kk & 3);
+    }
+    __device__ __forceinline__ void load(const RbArgs& a, const u32 tile, const u32 q0,
+                                         f32x4 (&bv)[NK]) {
+        const u32 l = __lane_id(), rr = l & 15, g = l >> 4;
+        const u32 p = a.tilePanel[tile].x;
+        const u32 c = a.denseCols[tile * 16 + rr];
+        const u32* bvals = a.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) idx[r] = bvals[16 * r];
-    const bool cvalid = c < a.N;
-    const float* arow = As + (p * 16 - q0 + rr) * LD + 4 * g;
-    const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * KT + 4 * g;
-    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-    constexpr int NK = KT / 16;
-    constexpr int CH = NK < 8 ? NK : 8;
+        for (int r = 0; r < 4; ++r) idx[r] = bvals[16 * r];
+        lr = p * 16 - q0 + rr;
+        const bool cvalid = c < a.N;
+        const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * KT;
 #pragma unroll
-    for (int k0 = 0; k0 < NK; k0 += CH) {
-        f32x4 bv[CH];
+        for (int kk = 0; kk < NK; ++kk) bv[kk] = cvalid ? ld4(bcol + 4 * chunk(kk, g)) : f32x4{0, 0, 0, 0};
+    }
+    __device__ __forceinline__ void run(const RbArgs& a, const float* As, const f32x4 (&bv)[NK]) const {
+        const u32 g = __lane_id() >> 4;
+        const float* arow = As + lr * KT;
+        f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-        for (int kk = 0; kk < CH; ++kk)
-            bv[kk] = cvalid ? ld4(bcol + 16 * (k0 + kk)) : f32x4{0, 0, 0, 0};
-#pragma unroll
-        for (int kk = 0; kk < CH; ++kk) {
-            const f32x4 av = *reinterpret_cast<const f32x4*>(arow + 16 * (k0 + kk));
+        for (int kk = 0; kk < NK; ++kk) {
+            const f32x4 av = *reinterpret_cast<const f32x4*>(arow + 4 * lds_chunk(lr, chunk(kk, g)));
             f32x4& acc = (kk & 1) ? acc1 : acc0;
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[kk].x, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[kk].y, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[kk].z, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[kk].w, acc, 0, 0, 0);
         }
-    }
-    const f32x4 acc = acc0 + acc1;
+        const f32x4 acc = acc0 + acc1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (idx[r] != NULLV) a.P[idx[r]] = acc[r];
+        for (int r = 0; r < 4; ++r)
+            if (idx[r] != NULLV) a.P[idx[r]] = acc[r];
+    }
+};
+
+// B pieces of the group's column (lane s: chunks 4 * ((f + j) mod NC) + s, f < NC)
+template <int KT>
+__device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const u32 sub,
+                                          const u32 (&rot)[KT / 16], f32x4 (&bv)[KT / 16]) {
+    const char* Bb = reinterpret_cast<const char*>(a.B);
+    const u32 bb = col * (KT * 4) + 16 * sub;
+#pragma unroll
+    for (u32 f = 0; f < KT / 16; ++f) bv[f] = *reinterpret_cast<const f32x4*>(Bb + (bb + rot[f]));
 }
 
-// residual entries [e0, e1) of the item; 64 row-groups (16 waves x 4) take contiguous shares
+// a column-run piece of a row-group: entries [first, first + len), len <= RB_PIECE_MAX = 16, all
+// in one column. Lane s of the group holds the metadata of entries first + 4k + s (k < 4).
+struct Piece {
+    u32 first, len;
+    u32 mm[4], mo[4];
+};
+
 template <int KT>
-__device__ __forceinline__ void residual_rb(const RbArgs& a, const u32 e0, const u32 e1,
-                                            const float* As, const u32 w) {
-    constexpr int W = KT >= 64 ? 4 : KT / 16;
-    constexpr int NF = KT / (16 * W);
-    constexpr int U = NF >= 8 ? 1 : 8 / NF;
-    constexpr u32 LD = KT + 4;
-    typedef typename vec<W>::t vt;
-    const u32 l = __lane_id(), sub = l & 15, grp = w * 4 + (l >> 4);
-    const u32 n = e1 - e0;
-    const u32 share = (n + 63) / 64;
-    const u32 gs = e0 + min(grp * share, n), ge = e0 + min(grp * share + share, n);
-    u32 curc = NULLV;
-    vt bcur[NF];
+__device__ __forceinline__ void load_piece(const RbArgs& a, const u32 pi, const u32 sub,
+                                           const u32 (&rot)[KT / 16], f32x4 (&bv)[KT / 16],
+                                           Piece& pc) {
+    const uint2 d = a.pieces[pi];
+    pc.first = d.x;
+    pc.len = (d.y >> 22) + 1;
+    load_bcol<KT>(a, d.y & 0x3FFFFFu, sub, rot, bv);
 #pragma unroll
-    for (int f = 0; f < NF; ++f) bcur[f] = vt{};
-    for (u32 base = gs; base < ge; base += 16) {
-        const u32 e = base + sub;
-        const bool okm = e < ge;
-        const u32 mmeta = okm ? a.meta[e] : NULLV;
-        const u32 mout = okm ? a.out[e] : 0u;
-        const u32 nb = min(16u, ge - base);
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 e = 4 * k + sub;
+        pc.mm[k] = e < pc.len ? a.meta[pc.first + e] : 0u;
+        pc.mo[k] = e < pc.len ? a.out[pc.first + e] : 0u;
+    }
+}
+
+// Step i of a batch of 4 computes entry 4k + i in all 4 lanes; lane i keeps it, so a batch ends
+// in one store instruction for 4 entries per group (64 outputs per full wave).
+template <int KT>
+__device__ __forceinline__ void residual_piece(const RbArgs& a, const float* As, const Piece& pc,
+                                               const u32 sub, const u32 (&rot)[KT / 16],
+                                               const f32x4 (&bv)[KT / 16]) {
+    constexpr u32 NC = KT / 16;
+    const char* Ab = reinterpret_cast<const char*>(As);
 #pragma unroll
-        for (int i0 = 0; i0 < 16; i0 += U) {
-            if (static_cast<u32>(i0) >= nb) break;
-            vt av[U][NF], bv[U][NF];
-            u32 cc[U], oo[U];
-            bool ok[U], chg[U];
+    for (u32 k = 0; k < 4; ++k) {
+        if (4 * k >= pc.len) break;
+        const u32 nb = min(4u, pc.len - 4 * k);
+        float res = 0.f;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                u32 m;
-                switch (i0 + u) {
-#define BSMR_B(I)                   \
-    case I:                         \
-        m = row_bcast<I>(mmeta);    \
-        oo[u] = row_bcast<I>(mout); \
-        break;
-                    BSMR_B(0) BSMR_B(1) BSMR_B(2) BSMR_B(3) BSMR_B(4) BSMR_B(5) BSMR_B(6) BSMR_B(7)
-                    BSMR_B(8) BSMR_B(9) BSMR_B(10) BSMR_B(11) BSMR_B(12) BSMR_B(13) BSMR_B(14)
-                    BSMR_B(15)
-#undef BSMR_B
-                    default:
-                        m = NULLV;
-                        oo[u] = 0;
-                }
-                ok[u] = static_cast<u32>(i0 + u) < nb;
-                cc[u] = m & 0x3FFFFFu;
-                const u32 lr = ok[u] ? (m >> 22) : 0u;
-                const u32 prev = u ? cc[u - 1] : curc;
-                chg[u] = ok[u] && cc[u] != prev;
-                const float* ap = As + lr * LD + W * sub;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) av[u][f] = *reinterpret_cast<const vt*>(ap + 16 * W * f);
-                if (chg[u]) {
-                    const float* bp = a.B + static_cast<size_t>(cc[u]) * KT + W * sub;
-#pragma unroll
-                    for (int f = 0; f < NF; ++f)
-                        bv[u][f] = *reinterpret_cast<const vt*>(bp + 16 * W * f);
-                }
+        for (int i = 0; i < 4; ++i) {
+            if (static_cast<u32>(i) >= nb) break;
+            u32 m;
+            switch (i) {
+                case 0: m = quad_bcast<0>(pc.mm[k]); break;
+                case 1: m = quad_bcast<1>(pc.mm[k]); break;
+                case 2: m = quad_bcast<2>(pc.mm[k]); break;
+                default: m = quad_bcast<3>(pc.mm[k]); break;
             }
+            const u32 lr = m >> 22;
+            const u32 ab = lr * (KT * 4) + 16 * (sub ^ (lr & 3));
+            f32x4 av[NC];  // all NC reads in flight before the first FMA
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!chg[u]) {
+            for (u32 f = 0; f < NC; ++f) av[f] = *reinterpret_cast<const f32x4*>(Ab + (ab + rot[f]));
+            f32x2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
 #pragma unroll
-                    for (int f = 0; f < NF; ++f) bv[u][f] = u ? bv[u - 1][f] : bcur[f];
-                }
-                float acc = 0.f;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) acc += vdot<W>(av[u][f], bv[u][f]);
-                acc = row_sum16(acc);
-                if (sub == 0 && ok[u]) a.P[oo[u]] = acc;
+            for (u32 f = 0; f < NC; ++f) {
+                acc0 = __builtin_elementwise_fma(f32x2{av[f].x, av[f].y}, f32x2{bv[f].x, bv[f].y}, acc0);
+                acc1 = __builtin_elementwise_fma(f32x2{av[f].z, av[f].w}, f32x2{bv[f].z, bv[f].w}, acc1);
             }
+            const f32x2 acc = acc0 + acc1;
+            float sm = acc.x + acc.y;
+            sm += dppf<0xB1>(sm);  // quad_perm [1,0,3,2]
+            sm += dppf<0x4E>(sm);  // quad_perm [2,3,0,1]
+            if (sub == static_cast<u32>(i)) res = sm;
+        }
+        if (sub < nb) a.P[pc.mo[k]] = res;
+    }
+}
+
+template <int KT, int NT>
+__global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float As[];
+    constexpr u32 NC = KT / 16;                             // chunks per lane (tile or row-group)
+    constexpr u32 NCH = KT / 4;                             // 16-byte chunks per row
+    constexpr u32 NW = NT / 64;                             // waves per workgroup
+    constexpr u32 SI = (160u * 1024u / 16u + NT - 1) / NT;  // staging chunks per thread (max)
+    const unsigned long long t0 = rtime(a.trace);
+    const uint4 it = a.items[blockIdx.x];
+    const u32 pend = a.itemEnd[blockIdx.x];
+    if (it.y == it.z && it.w == pend) return;  // padding item (uniform across the workgroup)
+    const u32 q0 = it.x * a.RB;
+    const u32 tid = threadIdx.x, w = tid >> 6, sub = tid & 3, j = (tid >> 2) & 15;
+    // every wave takes (at most) one dense tile and its 16 row-groups one residual piece each per
+    // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
+    // staging loads so all of it is in flight together
+    const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
+    const u32 np = (a.mode & 2) ? pend - it.w : 0u;
+    constexpr u32 NG = NT / 4;  // residual row-groups
+    const u32 gr = tid >> 2;
+    u32 rot[NC];  // residual: byte offset of the 64-byte quad the lane visits at step f
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (ok[u]) {
-                    curc = cc[u];
+    for (u32 f = 0; f < NC; ++f) rot[f] = 64u * ((f + j) % NC);
+    f32x4 tb[NC], pre[NC];
+    DenseTileLds<KT> dt;
+    // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
+    const u32 tw = NW - 1 - w;
+    if (tw < ntile) dt.load(a, it.y + tw, q0, tb);
+    Piece pc;
+    pc.len = 0;
+    if (gr < np) load_piece<KT>(a, it.w + gr, sub, rot, pre, pc);
+    // stage the row block in rounds of SH chunks per thread, all loads of a round in flight;
+    // the workgroups that stage the same block on one XCD start at different rows, so they do
+    // not all miss the L2 on the same lines at once
+    const u32 total = a.RB * NCH;
+    const u32 xoff = (a.diag & 16) ? 0u : ((blockIdx.x >> 3) * 37u % a.RB) * NCH;
+    constexpr u32 SH = 5;  // chunks per thread in flight per round (register budget)
 #pragma unroll
-                    for (int f = 0; f < NF; ++f) bcur[f] = bv[u][f];
-                }
+    for (u32 h = 0; h < (SI + SH - 1) / SH; ++h) {
+        f32x4 v[SH];
+#pragma unroll
+        for (u32 i = 0; i < SH; ++i) {
+            const u32 x0 = tid + (h * SH + i) * NT;
+            const u32 x = x0 + xoff >= total ? x0 + xoff - total : x0 + xoff;
+            const u32 lr = x / NCH, q = q0 + lr;
+            v[i] = (x0 < total && q < a.R)
+                       ? ld4(a.A + static_cast<size_t>(a.rows[q]) * KT + 4 * (x % NCH))
+                       : f32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (u32 i = 0; i < SH; ++i) {
+            const u32 x0 = tid + (h * SH + i) * NT;
+            if (x0 < total) {
+                const u32 x = x0 + xoff >= total ? x0 + xoff - total : x0 + xoff;
+                const u32 lr = x / NCH;
+                *reinterpret_cast<f32x4*>(As + lr * KT + 4 * lds_chunk(lr, x % NCH)) = v[i];
+            }
         }
     }
-}
-
-template <int KT>
-__global__ __launch_bounds__(1024) void k_sddmm_rb(RbArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float As[];
-    constexpr u32 LD = KT + 4, K4 = KT / 4;
-    const uint4 it = a.items[blockIdx.x];
-    const u32 q0 = it.x * a.RB;
-    const u32 tid = threadIdx.x;
-    for (u32 x = tid; x < a.RB * K4; x += 1024) {
-        const u32 lr = x / K4, k4 = x - lr * K4;
-        const u32 q = q0 + lr;
-        const f32x4 v = q < a.R ? ld4(a.A + static_cast<size_t>(a.rows[q]) * KT + 4 * k4)
-                                : f32x4{0, 0, 0, 0};
-        *reinterpret_cast<f32x4*>(As + lr * LD + 4 * k4) = v;
-    }
     __syncthreads();
-    const u32 w = tid >> 6;
-    if (a.mode & 1)
-        for (u32 t = it.y + w; t < it.z; t += 16) dense_tile_lds<KT>(a, t, As, q0);
-    if (a.mode & 2) residual_rb<KT>(a, it.w, a.itemEnd[blockIdx.x], As, w);
+    const unsigned long long tm = rtime(a.trace);
+    if (a.diag & 8) {  // staging only
+        trace_wave(a.trace, blockIdx.x * NW + w, t0, tm);
+        return;
+    }
+    if (tw < ntile) dt.run(a, As, tb);
+    const unsigned long long td = rtime(a.trace);
+    if (pc.len) residual_piece<KT>(a, As, pc, sub, rot, pre);
+    // later phases (items with more pieces than row-groups): the extra pieces are the shortest
+    // and go to the groups that had the shortest phase-0 pieces
+    for (u32 ph = 1; ph * NG < np; ++ph) {
+        const u32 pi = ph * NG + (NG - 1 - gr);
+        if (pi < np) {
+            load_piece<KT>(a, it.w + pi, sub, rot, pre, pc);
+            residual_piece<KT>(a, As, pc, sub, rot, pre);
+        }
+    }
+    for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
+        dt.load(a, t, q0, tb);
+        dt.run(a, As, tb);
+    }
+    trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
 }
 
 static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
@@ -581,11 +689,8 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
 int rb_slot(const Plan& p, u32 K) {
     if (p.N > (1u << 22) || !p.use_rowblock) return -1;
     switch (K) {
-        case 32: return 0;
-        case 64: return 1;
-        case 128: return 2;
-        case 256: return 3;
-        case 512: return 4;
+        case 64: return 0;
+        case 128: return 1;
         default: return -1;
     }
 }
@@ -611,29 +716,37 @@ int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP
     a.RB = L.RB;
     a.items = L.items.data();
     a.itemEnd = L.itemEnd.data();
+    a.pieces = L.pieces.data();
     a.meta = L.meta.data();
     a.out = L.out.data();
     a.tilePanel = p.denseItems.data();
     a.denseCols = p.denseCols.data();
     a.blockValues = p.blockValues.data();
     a.mode = mode;
-    const size_t lds = static_cast<size_t>(L.RB) * (L.K + 4) * sizeof(float);
-    void (*fn)(RbArgs) = nullptr;
-    switch (L.K) {
-        case 32: fn = k_sddmm_rb<32>; break;
-        case 64: fn = k_sddmm_rb<64>; break;
-        case 128: fn = k_sddmm_rb<128>; break;
-        case 256: fn = k_sddmm_rb<256>; break;
-        default: fn = k_sddmm_rb<512>; break;
+    a.diag = p.diag;
+    if (p.diag & 32) {
+        BSMR_CHECK(p.prepare_trace(static_cast<size_t>(L.nItems) * (L.NT / 64), s));
+        a.trace = p.trace.data();
     }
-    hipLaunchKernelGGL(fn, dim3(L.nItems), dim3(1024), lds, s, a);
+    void (*fn)(RbArgs) = nullptr;
+#define BSMR_RB(KT) (L.NT == 1024 ? k_sddmm_rb<KT, 1024> : k_sddmm_rb<KT, 512>)
+    switch (L.K) {
+        case 64: fn = BSMR_RB(64); break;
+        default: fn = BSMR_RB(128); break;
+    }
+#undef BSMR_RB
+    hipLaunchKernelGGL(fn, dim3(L.nItems), dim3(L.NT), L.lds, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }
 
-int launch_full(SddmmArgs a, hipStream_t s) {
+int launch_full(const Plan& p, SddmmArgs a, hipStream_t s) {
     const u32 items = a.nslots ? ((a.nd + 31) & ~31u) + a.nslots : a.nd;
     if (items == 0) return BSMR_OK;
+    if (p.diag & 32) {
+        BSMR_CHECK(p.prepare_trace((items + 3) / 4 * 4, s));
+        a.trace = p.trace.data();
+    }
     hipLaunchKernelGGL(pick_kernel<false>(a.K), dim3((items + 3) / 4), dim3(256), 0, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
@@ -670,7 +783,7 @@ extern "C" int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB,
     SddmmArgs a = make_args(p, dA, dB, K, dP);
     a.nd = p.nDenseItems;
     a.nslots = p.nSlots;
-    return launch_full(a, static_cast<hipStream_t>(stream));
+    return launch_full(p, a, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const void* dB,
@@ -737,7 +850,7 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     auto run = [&](u32 mode) -> int {
         if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, mode, s);
         if (slot >= 0) return launch_rb(p, slot, dA, dB, dP, mode, s);
-        return launch_full(mode == 1 ? dense : mode == 2 ? res : full, s);
+        return launch_full(p, mode == 1 ? dense : mode == 2 ? res : full, s);
     };
     BSMR_HIP(hipEventRecord(ev[0], s));
     for (int i = 0; i < iters; ++i) BSMR_CHECK(run(1));
@@ -755,5 +868,18 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     if (ms_residual) *ms_residual = p.nres ? t1 / iters : 0.f;
     if (ms_total) *ms_total = t2 / iters;
     for (auto& e : ev) (void)hipEventDestroy(e);
+    return BSMR_OK;
+}
+
+// debug timeline of the last traced launch (BSMR_DIAG & 32): 4 u64 per wave (not in the header)
+extern "C" int bsmr_debug_trace(const bsmr_plan* plan, uint64_t* host_out, uint64_t* len) {
+    if (!plan) return BSMR_ERR_INVALID;
+    const Plan& p = plan->p;
+    if (len) *len = p.traceN * 4ull;
+    if (host_out && p.traceN) {
+        BSMR_HIP(hipDeviceSynchronize());
+        BSMR_HIP(hipMemcpy(host_out, p.trace.data(), p.traceN * 4ull * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost));
+    }
     return BSMR_OK;
 }

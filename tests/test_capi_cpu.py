@@ -25,6 +25,18 @@ def test_library_exports_every_header_symbol():
     assert L.bsmr_abi_version() == 1
 
 
+def test_plan_options_defaults_and_struct_size():
+    """bsmr_plan_options_default fills exactly the ctypes mirror of the C struct."""
+    n = ctypes.sizeof(bsmr.PlanOptions)
+    buf = (ctypes.c_uint8 * (n + 32))(*([0xAB] * (n + 32)))
+    bsmr.lib().bsmr_plan_options_default(ctypes.cast(buf, ctypes.POINTER(bsmr.PlanOptions)))
+    assert bytes(buf[n:]) == b"\xab" * 32
+    o = bsmr.PlanOptions.from_buffer(buf)
+    assert abs(o.alpha - 0.3) < 1e-7 and abs(o.delta - 0.3) < 1e-7
+    assert (o.free_mem_bytes, o.device, o.cluster_batch, o.exact_similarity) == (0, 0, 0, 0)
+    assert (o.layout, o.lds_budget_kb) == (bsmr.LAYOUTS["auto"], 0)
+
+
 def test_make_data_known_answer():
     # reference makeData stream: A[0] = B[0] = 1.62944734 (single-threaded, SURVEY.md §8c)
     v = bsmr.make_data(4096)

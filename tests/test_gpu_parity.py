@@ -118,11 +118,12 @@ def test_nips_like_plan_bit_exact():
     assert_plans_equal(gp, op)
 
 
+@pytest.mark.parametrize("layout", ["auto", "colmajor"])
 @pytest.mark.parametrize("K", [16, 32, 48, 64, 96, 128, 256, 512])
 @pytest.mark.parametrize("delta", [0.0, 0.3, 1.1])
-def test_sddmm_values_checkdata(K, delta):
+def test_sddmm_values_checkdata(K, delta, layout):
     M, N, rp, ci = small_cases()["zipf"]
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=delta, free_mem_bytes=FREE)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=delta, free_mem_bytes=FREE, layout=layout)
     A = make_data(M * K)
     B = make_data(N * K)
     P = run_sddmm(plan, A, B, K, len(ci))
@@ -132,10 +133,14 @@ def test_sddmm_values_checkdata(K, delta):
     assert O.check_data(ref, P) == 0
 
 
-@pytest.mark.parametrize("K", [32, 128])
-def test_sddmm_nips_like_checkdata(K):
+@pytest.mark.parametrize("K,layout,lds_kb", [(32, "auto", 0), (64, "auto", 0), (128, "auto", 0),
+                                             (128, "colmajor", 0), (128, "auto", 48),
+                                             (256, "auto", 0), (512, "auto", 0),
+                                             (512, "auto", 160)])
+def test_sddmm_nips_like_checkdata(K, layout, lds_kb):
     M, N, rp, ci = nips_like_case()
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout=layout,
+                lds_budget_kb=lds_kb)
     A = make_data(M * K)
     B = make_data(N * K)
     P = run_sddmm(plan, A, B, K, len(ci))
@@ -143,11 +148,12 @@ def test_sddmm_nips_like_checkdata(K):
     assert O.check_data(ref, P) == 0
 
 
-def test_sddmm_blocky_dense_tiles():
+@pytest.mark.parametrize("K,layout", [(128, "auto"), (128, "colmajor"), (64, "auto"),
+                                      (256, "auto")])
+def test_sddmm_blocky_dense_tiles(K, layout):
     M, N, rp, ci = small_cases()["blocky"]
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout=layout)
     assert plan.stats()["num_dense_tiles"] > 0
-    K = 128
     A = make_data(M * K)
     B = make_data(N * K)
     P = run_sddmm(plan, A, B, K, len(ci))

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--workload", default="nips_like")
+    ap.add_argument("--layout", default="auto", choices=["auto", "rowblock", "colmajor"])
+    ap.add_argument("--lds-kb", type=int, default=0)
     args = ap.parse_args()
     import torch
 
@@ -27,7 +29,8 @@ def main():
 
     M, N, rp, ci = getattr(synth, args.workload)()
     K = args.K
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout,
+                lds_budget_kb=args.lds_kb)
     dA = torch.from_numpy(make_data(M * K)).cuda()
     dB = torch.from_numpy(make_data(N * K)).cuda()
     dP = torch.zeros(len(ci), dtype=torch.float32, device="cuda")
@@ -36,7 +39,8 @@ def main():
     r = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=args.iters, stream=s)
     torch.cuda.synchronize()
     st = plan.stats()
-    print(json.dumps({"M": M, "N": N, "nnz": len(ci), "K": K, "timing_ms": r,
+    print(json.dumps({"M": M, "N": N, "nnz": len(ci), "K": K, "layout": args.layout,
+                      "lds_kb": args.lds_kb, "timing_ms": r,
                       "dense_items": st["dense_items"], "residual_slots_hint": st["residual_items"],
                       "dense_tiles": st["num_dense_tiles"], "residual": st["num_residual"]}))
 
