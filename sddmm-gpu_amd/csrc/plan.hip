@@ -847,9 +847,10 @@ int Plan::build_rowblock_layout(int slot, u32 K) const {
         set_error("row-block layout needs N <= 2^22");
         return BSMR_ERR_UNSUPPORTED;
     }
-    const u32 RBr = rowblock_rows(K, rb_lds_kb, R);
+    const u32 KS = std::min<u32>(K, 128);  // k-slice staged in LDS (sddmm.hip)
+    const u32 RBr = rowblock_rows(KS, rb_lds_kb, R);
     const u32 nRB = (R + RBr - 1) / RBr;
-    const size_t lds = static_cast<size_t>(RBr) * K * sizeof(float);
+    const size_t lds = static_cast<size_t>(RBr) * KS * sizeof(float);
     const u32 NT = lds > 80 * 1024 ? 1024 : 512;
     const u32 wgPerCU = std::max<u32>(1, std::min<u32>(static_cast<u32>(160 * 1024 / lds), 2048 / NT));
     int cus = 256;

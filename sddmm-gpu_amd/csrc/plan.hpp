@@ -86,7 +86,7 @@ struct Plan {
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}
     };
-    static constexpr int N_RB_LAYOUTS = 2;  // K = 64, 128
+    static constexpr int N_RB_LAYOUTS = 4;  // K = 64, 128, 256, 512
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
     int build_rowblock_layout(int slot, u32 K) const;
 

@@ -542,7 +542,6 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     constexpr u32 NC = KT / 16;                             // chunks per lane (tile or row-group)
     constexpr u32 NCH = KT / 4;                             // 16-byte chunks per row
     constexpr u32 NW = NT / 64;                             // waves per workgroup
-    constexpr u32 SI = (160u * 1024u / 16u + NT - 1) / NT;  // staging chunks per thread (max)
     const unsigned long long t0 = rtime(a.trace);
     const uint4 it = a.items[blockIdx.x];
     const u32 pend = a.itemEnd[blockIdx.x];
@@ -567,31 +566,28 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     Piece pc;
     pc.len = 0;
     if (gr < np) load_piece<KT>(a, it.w + gr, sub, rot, pre, pc);
-    // stage the row block in rounds of SH chunks per thread, all loads of a round in flight;
-    // the workgroups that stage the same block on one XCD start at different rows, so they do
-    // not all miss the L2 on the same lines at once
-    const u32 total = a.RB * NCH;
-    const u32 xoff = (a.diag & 16) ? 0u : ((blockIdx.x >> 3) * 37u % a.RB) * NCH;
-    constexpr u32 SH = 5;  // chunks per thread in flight per round (register budget)
+    // stage the row block by LDS-DMA: each wave-instruction fills one contiguous KiB of the image
+    // (RPB rows); lane l supplies row lr = RPB * b + l / LPR at physical chunk pc = l % LPR, read
+    // from the logical chunk lds_chunk(lr, pc) of A[rows[q0 + lr]] (the XOR is an involution)
+    {
+        constexpr u32 LPR = KT / 4, RPB = 64 / LPR;
+        // KiB blocks per wave (max): NT = 512 is launched only for images <= 80 KiB
+        constexpr u32 MAXB = ((NT == 1024 ? 160u : 80u) + NW - 1) / NW;
+        const u32 lane = tid & 63, nblk = a.RB / RPB;
+        u32 src[MAXB];
 #pragma unroll
-    for (u32 h = 0; h < (SI + SH - 1) / SH; ++h) {
-        f32x4 v[SH];
-#pragma unroll
-        for (u32 i = 0; i < SH; ++i) {
-            const u32 x0 = tid + (h * SH + i) * NT;
-            const u32 x = x0 + xoff >= total ? x0 + xoff - total : x0 + xoff;
-            const u32 lr = x / NCH, q = q0 + lr;
-            v[i] = (x0 < total && q < a.R)
-                       ? ld4(a.A + static_cast<size_t>(a.rows[q]) * KT + 4 * (x % NCH))
-                       : f32x4{0, 0, 0, 0};
+        for (u32 i = 0; i < MAXB; ++i) {
+            const u32 b = w + i * NW, lr = b * RPB + lane / LPR, q = q0 + lr;
+            src[i] = (b < nblk && q < a.R) ? a.rows[q] : 0u;
         }
 #pragma unroll
-        for (u32 i = 0; i < SH; ++i) {
-            const u32 x0 = tid + (h * SH + i) * NT;
-            if (x0 < total) {
-                const u32 x = x0 + xoff >= total ? x0 + xoff - total : x0 + xoff;
-                const u32 lr = x / NCH;
-                *reinterpret_cast<f32x4*>(As + lr * KT + 4 * lds_chunk(lr, x % NCH)) = v[i];
+        for (u32 i = 0; i < MAXB; ++i) {
+            const u32 b = w + i * NW, lr = b * RPB + lane / LPR;
+            if (b < nblk) {
+                const float* g = a.A + static_cast<size_t>(src[i]) * KT + 4 * lds_chunk(lr, lane % LPR);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(As + 256 * b),
+                                                 16, 0, 0);
             }
         }
     }
