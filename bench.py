@@ -43,8 +43,14 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="C4 size factor")
     ap.add_argument("--mask", default="uniform", choices=["uniform", "block"], help="C5 mask")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-split", action="store_true",
+                    help="skip the cold steps and the dense/residual split launches (rocprof runs: "
+                         "every traced launch of the kernel is then a timed-region step)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary with hbm_bytes_per_launch for roofline.traffic")
+                    help="PMC summary with hbm_bytes_per_launch for roofline.traffic (default: "
+                         "profiles/traffic_<config>_K<K>.json when present)")
+    ap.add_argument("--cold-steps", type=int, default=20,
+                    help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
 
 
@@ -185,9 +191,29 @@ def main():
         ms = D.max_over_ranks(ms, dev)  # whole-job time = slowest rank
     ms_per_step = ms / args.steps
 
+    # cold: before each step a 512 MiB write evicts the Infinity Cache (MALL) and the L2s, so
+    # A, B and the plan come from HBM; only the SDDMM launch is inside the events
+    cold_ms = None
+    if args.cold_steps > 0 and not args.no_split:
+        junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+        evs = []
+        for i in range(args.cold_steps):
+            junk.fill_(i & 0xFF)
+            a0 = torch.cuda.Event(enable_timing=True)
+            a1 = torch.cuda.Event(enable_timing=True)
+            a0.record(stream)
+            step()
+            a1.record(stream)
+            evs.append((a0, a1))
+        torch.cuda.synchronize()
+        cold_ms = statistics.median(a.elapsed_time(b) for a, b in evs)
+        del junk
+        if dist is not None:
+            cold_ms = D.max_over_ranks(cold_ms, dev)
+
     # the same kernel split into its dense-tile-only and residual-only launches
-    prof = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=20, stream=sp,
-                        dtype=dtype)
+    prof = {} if args.no_split else plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+                                                  iters=20, stream=sp, dtype=dtype)
     P_gpu = dP.cpu().numpy()
 
     s = 4 if dtype == F32 else 2
@@ -196,15 +222,22 @@ def main():
     bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
     achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}_K{K}.json")
+    if os.path.exists(tj):
+        with open(tj) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
-    kern = {0: "k_sddmm_f32", 1: "k_sddmm_half<f16>", 2: "k_sddmm_half<bf16>"}[dtype]
+    # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
+    if dtype == F32 and K in (64, 128):
+        kern = f"k_sddmm_rb<{K},1024> (row-block LDS layout: dense-tile MFMA + residual)"
+    elif dtype == F32:
+        kern = f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)"
+    else:
+        kern = f"k_sddmm_half<{'f16' if dtype == 1 else 'bf16'}> (dense-tile MFMA + residual)"
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -235,11 +268,15 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": f"{kern}<{K}> (one launch: dense-tile MFMA + residual)",
+            "kernel": kern,
             "bytes_alg_per_launch": bytes_alg,
         },
         "kernels_ms": {k: round(v, 5) for k, v in prof.items()},
     }
+    if cold_ms is not None:
+        out["cold"] = {"ms_per_step": round(cold_ms, 5),
+                       "value": round(flops_rank * world / (cold_ms * 1e-3) / 1e9, 2),
+                       "note": "median of steps each preceded by a 512 MiB write (MALL evicted)"}
     if not args.no_cpu_baseline:
         if dtype == F32:
             Ar, Br = A, B
