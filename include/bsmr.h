@@ -43,10 +43,19 @@ int bsmr_abi_version(void);
 /* ------------------------------------------------------------------ host matrix input ---- */
 typedef struct bsmr_csr bsmr_csr;
 
-/* Replaces sparseMatrix::CSR<float>::initializeFromMatrixFile / initializeFromMtxFile
- * (src/Matrix.cpp:279-294, 398-480). Same acceptance/rejection rules and messages; verbose != 0
- * prints "sparseMatrix::CSR initialize from file : <f>" like the reference. */
+/* Replaces sparseMatrix::CSR<float>::initializeFromMtxFile (src/Matrix.cpp:398-480): .mtx/.mmio
+ * only. Same acceptance/rejection rules and messages; verbose != 0 prints
+ * "sparseMatrix::CSR initialize from file : <f>" like the reference. */
 int bsmr_csr_load_mtx(const char* path, int verbose, bsmr_csr** out);
+/* Replaces CSR::initializeFromSmtxFile (Matrix.cpp:296-371), the DLMC .smtx format: header
+ * "rows cols nnz", one line of row offsets, one line of column indices; values 1. */
+int bsmr_csr_load_smtx(const char* path, int verbose, bsmr_csr** out);
+/* Replaces CSR::initializeFromGraphDataset (Matrix.cpp:482-575), SNAP edge lists (.txt): node ids
+ * renumbered by first appearance, rows = cols = "Nodes:", nnz = "Edges:". */
+int bsmr_csr_load_snap(const char* path, int verbose, bsmr_csr** out);
+/* Replaces CSR::initializeFromMatrixFile (Matrix.cpp:279-294): dispatch on the last '.' suffix
+ * (.mtx/.mmio, .smtx, .txt); any other suffix prints "Error, file format is not supported". */
+int bsmr_csr_load(const char* path, int verbose, bsmr_csr** out);
 /* Wrap caller arrays (copied). */
 int bsmr_csr_create(uint32_t M, uint32_t N, uint32_t nnz, const uint32_t* rowptr,
                     const uint32_t* colidx, bsmr_csr** out);

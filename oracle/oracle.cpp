@@ -126,7 +126,7 @@ extern "C" orc_csr* orc_load_mtx(const char* path, int verbose) {
     const std::string file(path);
     const size_t dot = file.find_last_of('.');
     const std::string suffix = dot == std::string::npos ? std::string() : file.substr(dot);
-    if (suffix != ".mtx" && suffix != ".mmio") {  // Matrix.cpp:279-294 (.smtx/.txt: later rows)
+    if (suffix != ".mtx" && suffix != ".mmio") {  // Matrix.cpp:279-294 (.smtx/.txt: orc_load)
         std::cerr << "Error, file format is not supported : " << file << std::endl;
         return nullptr;
     }
@@ -210,6 +210,189 @@ extern "C" orc_csr* orc_load_mtx(const char* path, int verbose) {
     }
     csr_offsets(M, rs, c->rowptr);
     return c;
+}
+
+// .smtx (DLMC), Matrix.cpp:296-371: '%' lines skipped; header "rows cols nnz"; nnz == 0 is
+// rejected; the next line holds rows+1 row offsets, the line after it nnz column indices, both
+// word-split as above; values are 1; a column repeated inside a row is rejected. Column order in a
+// row = file order. The reference throws on a missing or non-numeric word (that is how a short
+// line ends there) and does not validate the offsets or the column range; this restatement rejects
+// all of those with the messages below (documented deviations).
+extern "C" orc_csr* orc_load_smtx(const char* path, int verbose) {
+    const std::string file(path);
+    std::ifstream in(file);
+    if (!in.is_open()) {
+        std::cerr << "Error, file cannot be opened : " << file << std::endl;
+        return nullptr;
+    }
+    if (verbose) std::cout << "sparseMatrix::CSR initialize From file : " << file << std::endl;
+    std::string line;
+    bool got = false;
+    while (std::getline(in, line)) {
+        got = true;
+        if (line.empty() || line[0] != '%') break;
+    }
+    long hdr[3];
+    size_t it = 0;
+    for (long& h : hdr)
+        if (!got || !parse_int(next_word(line, it), h) || h < 0) {
+            std::cerr << "Error, file " << file << " format is incorrect!" << std::endl;
+            return nullptr;
+        }
+    const u32 M = static_cast<u32>(hdr[0]), N = static_cast<u32>(hdr[1]), nnz = static_cast<u32>(hdr[2]);
+    if (nnz == 0) {
+        std::cerr << "Error, file " << file << " nnz is 0!" << std::endl;
+        return nullptr;
+    }
+    auto* c = new orc_csr;
+    c->M = M;
+    c->N = N;
+    c->nnz = nnz;
+    c->rowptr.resize(static_cast<size_t>(M) + 1);
+    c->col.resize(nnz);
+    c->val.assign(nnz, 1.f);
+    auto fail = [&](const std::string& msg) {
+        std::cerr << msg << std::endl;
+        delete c;
+        return static_cast<orc_csr*>(nullptr);
+    };
+    auto read_ints = [&](std::vector<u32>& dst) {
+        if (!std::getline(in, line)) return false;
+        size_t w = 0;
+        for (u32& v : dst) {
+            long x;
+            if (!parse_int(next_word(line, w), x) || x < 0) return false;
+            v = static_cast<u32>(x);
+        }
+        return true;
+    };
+    if (!read_ints(c->rowptr)) return fail("Error, file " + file + " rowOffsets is not enough!");
+    if (!read_ints(c->col)) return fail("Error, file " + file + " nnz is not enough!");
+    if (c->rowptr[0] != 0 || c->rowptr[M] != nnz) return fail("Error, file " + file + " format is incorrect!");
+    for (u32 r = 0; r < M; ++r)
+        if (c->rowptr[r] > c->rowptr[r + 1]) return fail("Error, file " + file + " format is incorrect!");
+    for (u32 r = 0; r < M; ++r) {
+        std::set<u32> seen;
+        for (u32 k = c->rowptr[r]; k < c->rowptr[r + 1]; ++k) {
+            if (c->col[k] >= N) return fail("Error, file " + file + " row or col is too big!");
+            if (!seen.insert(c->col[k]).second) return fail("Error, matrix has duplicate data!");
+        }
+    }
+    return c;
+}
+
+// SNAP edge list (.txt), Matrix.cpp:482-575: leading '#' lines, of which one carries
+// "Nodes: <n>" and one "Edges: <e>" (possibly the same line); rows = cols = n, nnz = e. Then one
+// "from to [value]" per line (blank lines skipped); node ids are renumbered 0, 1, .. in order of
+// first appearance (from before to); more than e edges, fewer, an id >= n or a repeated
+// (from, to) pair is rejected, the first offending edge in file order deciding the message; the
+// edges are then stably sorted by row (file order inside a row). No mirroring.
+extern "C" orc_csr* orc_load_snap(const char* path, int verbose) {
+    const std::string file(path);
+    std::ifstream in(file);
+    if (!in.is_open()) {
+        std::cerr << "Error, file cannot be opened : " << file << std::endl;
+        return nullptr;
+    }
+    if (verbose) std::cout << "sparseMatrix::CSR initialize From file : " << file << std::endl;
+    std::string line;
+    long nodes = 0, edges = 0;
+    bool data = false;  // `line` holds the first data line
+    while (std::getline(in, line)) {
+        if (line.empty() || line[0] != '#') {
+            data = true;
+            break;
+        }
+        for (const char* key : {"Nodes: ", "Edges: "}) {
+            const size_t at = line.find(key);
+            if (at == std::string::npos) continue;
+            size_t w = at + 7;
+            long v;
+            if (!parse_int(next_word(line, w), v) || v < 0) {
+                std::cerr << "Error, file " << file << " format is incorrect!" << std::endl;
+                return nullptr;
+            }
+            (key[0] == 'N' ? nodes : edges) = v;
+        }
+    }
+    if (!nodes || !edges) {
+        std::cerr << "Error, file " << file << " row or col or nnz not initialized!" << std::endl;
+        return nullptr;
+    }
+    const u32 n = static_cast<u32>(nodes), e = static_cast<u32>(edges);
+    std::vector<u32> ri, ci;
+    std::vector<float> vv;
+    std::unordered_map<u32, u32> id;
+    auto renum = [&](u32 node) {
+        auto f = id.find(node);
+        if (f != id.end()) return f->second;
+        const u32 k = static_cast<u32>(id.size());
+        id.emplace(node, k);
+        return k;
+    };
+    for (bool have = data; have; have = static_cast<bool>(std::getline(in, line))) {
+        u32 a, b;
+        float v = 0.f;
+        const int st = three_words(line, a, b, v);
+        if (st == 0) continue;
+        if (st < 0) {
+            std::cerr << "Error, file " << file << " format is incorrect!" << std::endl;
+            return nullptr;
+        }
+        const u32 ra = renum(a), rb = renum(b);
+        if (ri.size() >= e) {
+            std::cerr << "Error, file " << file << " too many elements, exceeding the number nnz!"
+                      << std::endl;
+            return nullptr;
+        }
+        ri.push_back(ra);
+        ci.push_back(rb);
+        vv.push_back(v);
+    }
+    if (ri.size() < e) {
+        std::cerr << "Error, file " << file << " elements is not enough!" << std::endl;
+        return nullptr;
+    }
+    std::set<std::pair<u32, u32>> seen;
+    for (u32 i = 0; i < e; ++i) {
+        if (ri[i] >= n || ci[i] >= n) {
+            std::cerr << "Error, file " << file << " row or col is too big!" << std::endl;
+            return nullptr;
+        }
+        if (!seen.insert({ri[i], ci[i]}).second) {
+            std::cerr << "Error, matrix has duplicate data!" << std::endl;
+            return nullptr;
+        }
+    }
+    std::vector<u32> order(e);
+    for (u32 i = 0; i < e; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](u32 x, u32 y) { return ri[x] < ri[y]; });
+    auto* c = new orc_csr;
+    c->M = n;
+    c->N = n;
+    c->nnz = e;
+    c->col.resize(e);
+    c->val.resize(e);
+    std::vector<u32> rs(e);
+    for (u32 i = 0; i < e; ++i) {
+        rs[i] = ri[order[i]];
+        c->col[i] = ci[order[i]];
+        c->val[i] = vv[order[i]];
+    }
+    csr_offsets(n, rs, c->rowptr);
+    return c;
+}
+
+// CSR::initializeFromMatrixFile (Matrix.cpp:279-294): dispatch on the last '.' suffix
+extern "C" orc_csr* orc_load(const char* path, int verbose) {
+    const std::string file(path);
+    const size_t dot = file.find_last_of('.');
+    const std::string suffix = dot == std::string::npos ? std::string() : file.substr(dot);
+    if (suffix == ".mtx" || suffix == ".mmio") return orc_load_mtx(path, verbose);
+    if (suffix == ".smtx") return orc_load_smtx(path, verbose);
+    if (suffix == ".txt") return orc_load_snap(path, verbose);
+    std::cerr << "Error, file format is not supported : " << file << std::endl;
+    return nullptr;
 }
 
 extern "C" orc_csr* orc_csr_from_arrays(uint32_t M, uint32_t N, uint32_t nnz,

@@ -30,6 +30,9 @@ typedef struct orc_plan orc_plan;
 /* ---- Matrix Market loader (Matrix.cpp:279-294, 373-480; util.hpp:182-197) ---- */
 /* Returns NULL on any rejection the reference makes; prints the reference messages. */
 orc_csr* orc_load_mtx(const char* path, int verbose);
+orc_csr* orc_load_smtx(const char* path, int verbose);  // Matrix.cpp:296-371
+orc_csr* orc_load_snap(const char* path, int verbose);  // Matrix.cpp:482-575
+orc_csr* orc_load(const char* path, int verbose);       // suffix dispatch, Matrix.cpp:279-294
 orc_csr* orc_csr_from_arrays(uint32_t M, uint32_t N, uint32_t nnz, const uint32_t* rowptr,
                              const uint32_t* colidx);
 void orc_csr_info(const orc_csr* c, uint32_t* M, uint32_t* N, uint32_t* nnz);

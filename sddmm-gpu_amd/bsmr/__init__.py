@@ -73,7 +73,8 @@ class EvalStats(C.Structure):
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
-    "bsmr_last_error", "bsmr_abi_version", "bsmr_csr_load_mtx", "bsmr_csr_create",
+    "bsmr_last_error", "bsmr_abi_version", "bsmr_csr_load_mtx", "bsmr_csr_load_smtx",
+    "bsmr_csr_load_snap", "bsmr_csr_load", "bsmr_csr_create",
     "bsmr_csr_info", "bsmr_csr_rowptr", "bsmr_csr_colidx", "bsmr_csr_values", "bsmr_csr_free",
     "bsmr_make_data", "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
     "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
@@ -102,7 +103,8 @@ def lib():
     vp = C.c_void_p
     L.bsmr_last_error.restype = C.c_char_p
     L.bsmr_abi_version.restype = C.c_int
-    L.bsmr_csr_load_mtx.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+    for f in ("bsmr_csr_load_mtx", "bsmr_csr_load_smtx", "bsmr_csr_load_snap", "bsmr_csr_load"):
+        getattr(L, f).argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
     L.bsmr_csr_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p, C.POINTER(vp)]
     L.bsmr_csr_info.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                 C.POINTER(C.c_uint32)]
@@ -159,8 +161,17 @@ class Csr:
 
     @classmethod
     def load_mtx(cls, path, verbose=False):
+        return cls._load("bsmr_csr_load_mtx", path, verbose)
+
+    @classmethod
+    def load(cls, path, verbose=False):
+        """Any supported file (.mtx/.mmio, .smtx, SNAP .txt) by suffix; None if rejected."""
+        return cls._load("bsmr_csr_load", path, verbose)
+
+    @classmethod
+    def _load(cls, fn, path, verbose):
         h = C.c_void_p()
-        st = lib().bsmr_csr_load_mtx(path.encode(), 1 if verbose else 0, C.byref(h))
+        st = getattr(lib(), fn)(path.encode(), 1 if verbose else 0, C.byref(h))
         if st != 0:
             return None
         return cls(h)
@@ -194,6 +205,10 @@ class Csr:
 
 def load_mtx(path, verbose=False):
     return Csr.load_mtx(path, verbose)
+
+
+def load(path, verbose=False):
+    return Csr.load(path, verbose)
 
 
 class Plan:

@@ -208,3 +208,24 @@ def write_mtx(path, M, N, rowptr, colidx, symmetric_header=False):
         f.write(f"{M} {N} {nnz}\n")
         data = np.stack([rows + 1, colidx.astype(np.int64) + 1], axis=1)
         np.savetxt(f, data, fmt="%d")
+
+
+def write_smtx(path, M, N, rowptr, colidx):
+    """Write a DLMC .smtx file: header "M, N, nnz" words, one line of row offsets, one of column
+    indices (the format CSR::initializeFromSmtxFile reads, src/Matrix.cpp:296-371)."""
+    with open(path, "w") as f:
+        f.write(f"{M} {N} {int(rowptr[-1])}\n")
+        f.write(" ".join(str(int(x)) for x in rowptr) + "\n")
+        f.write(" ".join(str(int(x)) for x in colidx) + "\n")
+
+
+def write_snap(path, M, rowptr, colidx, id_base=1):
+    """Write a square pattern as a SNAP edge list ("# Nodes:"/"# Edges:" header, "from\\tto" per
+    line). Node ids are id_base + index; the loader renumbers them by first appearance, so the
+    loaded matrix is a symmetric permutation of this one (CSR::initializeFromGraphDataset)."""
+    nnz = int(rowptr[-1])
+    rows = np.repeat(np.arange(M, dtype=np.int64), np.diff(rowptr.astype(np.int64)))
+    with open(path, "w") as f:
+        f.write(f"# Directed graph: {path}\n# Nodes: {M} Edges: {nnz}\n# FromNodeId\tToNodeId\n")
+        data = np.stack([rows + id_base, colidx.astype(np.int64) + id_base], axis=1)
+        np.savetxt(f, data, fmt="%d", delimiter="\t")

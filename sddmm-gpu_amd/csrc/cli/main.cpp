@@ -130,7 +130,7 @@ void base_fields(const cli::Options& o, const bsmr_csr* S, uint32_t K, cli::Logg
 int main(int argc, char* argv[]) {
     cli::Options options(argc, argv);
     bsmr_csr* S = nullptr;
-    if (bsmr_csr_load_mtx(options.inputFile().c_str(), 1, &S) != BSMR_OK) {
+    if (bsmr_csr_load(options.inputFile().c_str(), 1, &S) != BSMR_OK) {
         fprintf(stderr, "Error, matrix S initialize failed.\n");
         return -1;
     }

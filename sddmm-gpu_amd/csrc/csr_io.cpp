@@ -23,6 +23,7 @@
 #include <random>
 #include <sstream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "common.hpp"
@@ -218,6 +219,233 @@ extern "C" int bsmr_csr_load_mtx(const char* path, int verbose, bsmr_csr** out) 
     }
     *out = s;
     return BSMR_OK;
+}
+
+namespace {
+
+// whole-file line reader ('\n'-separated; '\r' is a word separator as in the reference)
+struct Lines {
+    std::string buf;
+    const char* p = nullptr;
+    const char* end = nullptr;
+    bool open(const std::string& file) {
+        std::ifstream in(file, std::ios::binary);
+        if (!in.is_open()) return false;
+        buf.assign((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        p = buf.data();
+        end = p + buf.size();
+        return true;
+    }
+    bool next(const char*& lb, const char*& le) {
+        if (p >= end) return false;
+        lb = p;
+        const char* nl = static_cast<const char*>(std::memchr(p, '\n', end - p));
+        le = nl ? nl : end;
+        p = nl ? nl + 1 : end;
+        return true;
+    }
+};
+
+int reject_msg(const std::string& msg, int code) {
+    std::cerr << msg << std::endl;
+    set_error(msg);
+    return code;
+}
+
+// stable counting sort of (row, col, value) triples into CSR (file order kept inside a row)
+bsmr_csr* to_csr(uint32_t M, uint32_t N, const std::vector<uint32_t>& ri,
+                 const std::vector<uint32_t>& ci, const std::vector<float>& vv) {
+    auto* s = new bsmr_csr;
+    s->M = M;
+    s->N = N;
+    s->nnz = static_cast<uint32_t>(ri.size());
+    s->rowptr.assign(static_cast<size_t>(M) + 1, 0);
+    for (uint32_t r : ri) ++s->rowptr[r + 1];
+    for (uint32_t r = 0; r < M; ++r) s->rowptr[r + 1] += s->rowptr[r];
+    std::vector<uint32_t> fill(s->rowptr.begin(), s->rowptr.end() - 1);
+    s->colidx.resize(ri.size());
+    s->values.resize(ri.size());
+    for (size_t i = 0; i < ri.size(); ++i) {
+        const uint32_t dst = fill[ri[i]]++;
+        s->colidx[dst] = ci[i];
+        s->values[dst] = vv[i];
+    }
+    return s;
+}
+
+// index of the first entry (in file order) that repeats an earlier (row, col) pair, or n
+size_t first_duplicate(const std::vector<uint32_t>& ri, const std::vector<uint32_t>& ci, size_t n) {
+    std::vector<uint32_t> ord(n);
+    std::iota(ord.begin(), ord.end(), 0u);
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+        if (ri[a] != ri[b]) return ri[a] < ri[b];
+        if (ci[a] != ci[b]) return ci[a] < ci[b];
+        return a < b;
+    });
+    size_t first = n;
+    for (size_t k = 1; k < n; ++k)
+        if (ri[ord[k]] == ri[ord[k - 1]] && ci[ord[k]] == ci[ord[k - 1]]) first = std::min<size_t>(first, ord[k]);
+    return first;
+}
+
+}  // namespace
+
+// .smtx (DLMC) — CSR::initializeFromSmtxFile (src/Matrix.cpp:296-371): '%' lines skipped, header
+// "rows cols nnz" (nnz == 0 rejected), one line of rows+1 row offsets, one line of nnz column
+// indices, values 1, a column repeated inside a row rejected, column order = file order.
+// Deviations (the reference throws on a short or non-numeric line and does not validate the
+// offsets or the column range): all rejected with the messages below.
+extern "C" int bsmr_csr_load_smtx(const char* path, int verbose, bsmr_csr** out) {
+    *out = nullptr;
+    const std::string file(path ? path : "");
+    Lines L;
+    if (!L.open(file)) return reject_msg("Error, file cannot be opened : " + file, BSMR_ERR_IO);
+    if (verbose) std::cout << "sparseMatrix::CSR initialize From file : " << file << std::endl;
+    const char *lb = nullptr, *le = nullptr;
+    bool got = false;
+    while (L.next(lb, le)) {
+        got = true;
+        if (lb == le || *lb != '%') break;
+    }
+    long hdr[3];
+    {
+        Words it{lb, le};
+        std::string w;
+        for (long& h : hdr) {
+            it.next(w);
+            if (!got || !to_int(w, h) || h < 0)
+                return reject_msg("Error, file " + file + " format is incorrect!", BSMR_ERR_IO);
+        }
+    }
+    const uint32_t M = static_cast<uint32_t>(hdr[0]), N = static_cast<uint32_t>(hdr[1]);
+    const uint32_t nnz = static_cast<uint32_t>(hdr[2]);
+    if (nnz == 0) return reject_msg("Error, file " + file + " nnz is 0!", BSMR_ERR_REJECTED);
+    auto read_ints = [&](std::vector<uint32_t>& dst) {
+        if (!L.next(lb, le)) return false;
+        Words it{lb, le};
+        std::string w;
+        for (uint32_t& v : dst) {
+            long x;
+            it.next(w);
+            if (!to_int(w, x) || x < 0) return false;
+            v = static_cast<uint32_t>(x);
+        }
+        return true;
+    };
+    auto* s = new bsmr_csr;
+    s->M = M;
+    s->N = N;
+    s->nnz = nnz;
+    s->rowptr.resize(static_cast<size_t>(M) + 1);
+    s->colidx.resize(nnz);
+    s->values.assign(nnz, 1.f);
+    auto fail = [&](const std::string& msg, int code) {
+        delete s;
+        return reject_msg(msg, code);
+    };
+    if (!read_ints(s->rowptr)) return fail("Error, file " + file + " rowOffsets is not enough!", BSMR_ERR_IO);
+    if (!read_ints(s->colidx)) return fail("Error, file " + file + " nnz is not enough!", BSMR_ERR_IO);
+    if (s->rowptr[0] != 0 || s->rowptr[M] != nnz)
+        return fail("Error, file " + file + " format is incorrect!", BSMR_ERR_IO);
+    for (uint32_t r = 0; r < M; ++r)
+        if (s->rowptr[r] > s->rowptr[r + 1]) return fail("Error, file " + file + " format is incorrect!", BSMR_ERR_IO);
+    std::vector<uint32_t> mark(N, NULLV);  // last row that used column c
+    for (uint32_t r = 0; r < M; ++r)
+        for (uint32_t k = s->rowptr[r]; k < s->rowptr[r + 1]; ++k) {
+            const uint32_t c = s->colidx[k];
+            if (c >= N) return fail("Error, file " + file + " row or col is too big!", BSMR_ERR_REJECTED);
+            if (mark[c] == r) return fail("Error, matrix has duplicate data!", BSMR_ERR_REJECTED);
+            mark[c] = r;
+        }
+    *out = s;
+    return BSMR_OK;
+}
+
+// SNAP edge list (.txt) — CSR::initializeFromGraphDataset (src/Matrix.cpp:482-575): leading '#'
+// lines carry "Nodes: n" and "Edges: e" (rows = cols = n, nnz = e); then "from to [value]" lines
+// (blank skipped); node ids renumbered 0, 1, .. by first appearance (from, then to); more than e
+// edges, fewer, an id >= n or a repeated pair rejected (first offending edge in file order
+// decides); stable sort by row. No mirroring (directed edges as listed).
+extern "C" int bsmr_csr_load_snap(const char* path, int verbose, bsmr_csr** out) {
+    *out = nullptr;
+    const std::string file(path ? path : "");
+    Lines L;
+    if (!L.open(file)) return reject_msg("Error, file cannot be opened : " + file, BSMR_ERR_IO);
+    if (verbose) std::cout << "sparseMatrix::CSR initialize From file : " << file << std::endl;
+    const char *lb = nullptr, *le = nullptr;
+    long nodes = 0, edges = 0;
+    bool data = false;
+    while (L.next(lb, le)) {
+        if (lb == le || *lb != '#') {
+            data = true;
+            break;
+        }
+        const std::string line(lb, le);
+        for (const char* key : {"Nodes: ", "Edges: "}) {
+            const size_t at = line.find(key);
+            if (at == std::string::npos) continue;
+            Words it{line.data() + at + 7, line.data() + line.size()};
+            std::string w;
+            it.next(w);
+            long v;
+            if (!to_int(w, v) || v < 0) return reject_msg("Error, file " + file + " format is incorrect!", BSMR_ERR_IO);
+            (key[0] == 'N' ? nodes : edges) = v;
+        }
+    }
+    if (!nodes || !edges)
+        return reject_msg("Error, file " + file + " row or col or nnz not initialized!", BSMR_ERR_REJECTED);
+    const uint32_t n = static_cast<uint32_t>(nodes), e = static_cast<uint32_t>(edges);
+    std::vector<uint32_t> ri, ci;
+    std::vector<float> vv;
+    ri.reserve(e);
+    ci.reserve(e);
+    vv.reserve(e);
+    std::unordered_map<uint32_t, uint32_t> id;
+    auto renum = [&](uint32_t node) {
+        const auto ins = id.emplace(node, static_cast<uint32_t>(id.size()));
+        return ins.first->second;
+    };
+    for (bool have = data; have; have = L.next(lb, le)) {
+        uint32_t a = 0, b = 0;
+        float v = 0.f;
+        const int st = parse_line(lb, le, a, b, v);
+        if (st == 0) continue;
+        if (st < 0) return reject_msg("Error, file " + file + " format is incorrect!", BSMR_ERR_IO);
+        const uint32_t ra = renum(a), rb = renum(b);
+        if (ri.size() >= e)
+            return reject_msg("Error, file " + file + " too many elements, exceeding the number nnz!",
+                              BSMR_ERR_REJECTED);
+        ri.push_back(ra);
+        ci.push_back(rb);
+        vv.push_back(v);
+    }
+    if (ri.size() < e) return reject_msg("Error, file " + file + " elements is not enough!", BSMR_ERR_REJECTED);
+    size_t first_oob = e;
+    for (size_t i = 0; i < e; ++i)
+        if (ri[i] >= n || ci[i] >= n) {
+            first_oob = i;
+            break;
+        }
+    // a repeat before the first out-of-range edge decides first (== first_oob: no repeat there)
+    if (first_duplicate(ri, ci, first_oob) < first_oob)
+        return reject_msg("Error, matrix has duplicate data!", BSMR_ERR_REJECTED);
+    if (first_oob < e) return reject_msg("Error, file " + file + " row or col is too big!", BSMR_ERR_REJECTED);
+    *out = to_csr(n, n, ri, ci, vv);
+    return BSMR_OK;
+}
+
+// CSR::initializeFromMatrixFile (src/Matrix.cpp:279-294): dispatch on the last '.' suffix
+extern "C" int bsmr_csr_load(const char* path, int verbose, bsmr_csr** out) {
+    *out = nullptr;
+    const std::string file(path ? path : "");
+    const size_t dot = file.find_last_of('.');
+    const std::string suffix = dot == std::string::npos ? std::string() : file.substr(dot);
+    if (suffix == ".mtx" || suffix == ".mmio") return bsmr_csr_load_mtx(path, verbose, out);
+    if (suffix == ".smtx") return bsmr_csr_load_smtx(path, verbose, out);
+    if (suffix == ".txt") return bsmr_csr_load_snap(path, verbose, out);
+    std::cerr << "Error, file format is not supported : " << file << std::endl;
+    set_error("unsupported file suffix: " + file);
+    return BSMR_ERR_UNSUPPORTED;
 }
 
 extern "C" int bsmr_csr_create(uint32_t M, uint32_t N, uint32_t nnz, const uint32_t* rowptr,

@@ -50,8 +50,9 @@ def lib():
             import subprocess
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
         L = C.CDLL(LIB_PATH)
-        L.orc_load_mtx.restype = C.c_void_p
-        L.orc_load_mtx.argtypes = [C.c_char_p, C.c_int]
+        for f in ("orc_load_mtx", "orc_load_smtx", "orc_load_snap", "orc_load"):
+            getattr(L, f).restype = C.c_void_p
+            getattr(L, f).argtypes = [C.c_char_p, C.c_int]
         L.orc_csr_from_arrays.restype = C.c_void_p
         L.orc_csr_from_arrays.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p]
         L.orc_csr_info.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -95,7 +96,7 @@ class CSR:
 
     @classmethod
     def load(cls, path, verbose=False):
-        h = lib().orc_load_mtx(path.encode(), 1 if verbose else 0)
+        h = lib().orc_load(path.encode(), 1 if verbose else 0)  # suffix dispatch
         return cls(h) if h else None
 
     @classmethod

@@ -100,6 +100,24 @@ def test_cli_default_run_log(tmp_path):
     assert re.search(r"\[bsmr_gflops : [0-9.]+\]", r.stdout)
 
 
+@pytest.mark.parametrize("fmt", ["smtx", "snap"])
+def test_cli_other_formats(tmp_path, fmt):
+    """.smtx (DLMC) and SNAP .txt inputs through the CLI's suffix dispatch: checkData passes."""
+    M, N, rp, ci = synth.random_rows(400, 400, 30, seed=12, zipf=1.05)
+    if fmt == "smtx":
+        path = str(tmp_path / "s.smtx")
+        synth.write_smtx(path, M, N, rp, ci)
+    else:
+        path = str(tmp_path / "s.txt")
+        synth.write_snap(path, M, rp, ci)
+    r = subprocess.run([BIN, "-f", path, "-k", "128"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert f"sparseMatrix::CSR initialize From file : {path}" in r.stdout
+    f = _log_fields(r.stdout)
+    assert f["NNZ"] == str(len(ci)) and f["K"] == "128"
+    assert "NO PASS" not in r.stdout
+
+
 def test_cli_positional_and_failure(tmp_path):
     M, N, rp, ci = synth.random_rows(100, 300, 10, seed=10)
     path = str(tmp_path / "p.mtx")
