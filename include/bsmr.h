@@ -161,6 +161,12 @@ int bsmr_plan_evaluate(const bsmr_plan* plan, bsmr_eval_stats* out);
  * with fp32 accumulation). stream: a hipStream_t (NULL = default stream). Asynchronous. */
 int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K, int dtype,
                float* dP, void* stream);
+/* Replaces sddmm_gpu_batch(numBatch, M, N, K, nnz, dA, dB, rphm, dP, time)
+ * (include/sddmmKernel.cuh:41-47, src/sddmmKernel.cu:2764-2850): the same plan over num_batch
+ * (A, B) pairs, batch b at dA + b*M*K, dB + b*N*K elements, writing dP + b*nnz (the reference's
+ * batch strides, sddmmKernel.cu:1281-1283). One launch per 65535 batches. Asynchronous. */
+int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const void* dA, const void* dB,
+                     uint32_t K, int dtype, float* dP, void* stream);
 
 /* Row-panel sharding for multi-GPU runs: contiguous panel ranges balanced by a
  * cost model; bsmr_sddmm_panels computes only the outputs of panels [p0, p1). */

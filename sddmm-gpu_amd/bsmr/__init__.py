@@ -78,7 +78,7 @@ EXPORTS = [
     "bsmr_csr_info", "bsmr_csr_rowptr", "bsmr_csr_colidx", "bsmr_csr_values", "bsmr_csr_free",
     "bsmr_make_data", "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
     "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
-    "bsmr_sddmm", "bsmr_plan_shard", "bsmr_shard_cuts", "bsmr_sddmm_panels",
+    "bsmr_sddmm", "bsmr_sddmm_batch", "bsmr_plan_shard", "bsmr_shard_cuts", "bsmr_sddmm_panels",
     "bsmr_sddmm_profile",
 ]
 
@@ -125,6 +125,7 @@ def lib():
     L.bsmr_plan_get_array.argtypes = [vp, C.c_int, vp, C.POINTER(C.c_uint64)]
     L.bsmr_plan_evaluate.argtypes = [vp, C.POINTER(EvalStats)]
     L.bsmr_sddmm.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, vp]
+    L.bsmr_sddmm_batch.argtypes = [vp, C.c_uint32, vp, vp, C.c_uint32, C.c_int, vp, vp]
     L.bsmr_plan_shard.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32),
                                   C.POINTER(C.c_uint32)]
     L.bsmr_shard_cuts.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_int, _u32p]
@@ -260,6 +261,11 @@ class Plan:
     def sddmm(self, dA, dB, K, dP, stream=0, dtype=F32):
         """dA, dB, dP: device pointers (int) — e.g. torch tensor .data_ptr()."""
         _check(lib().bsmr_sddmm(self.h, dA, dB, K, dtype, dP, stream or None), "bsmr_sddmm")
+
+    def sddmm_batch(self, num_batch, dA, dB, K, dP, stream=0, dtype=F32):
+        """num_batch (A, B) pairs: batch b at dA + b*M*K, dB + b*N*K elements, dP + b*nnz."""
+        _check(lib().bsmr_sddmm_batch(self.h, num_batch, dA, dB, K, dtype, dP, stream or None),
+               "bsmr_sddmm_batch")
 
     def sddmm_panels(self, dA, dB, K, dP, p0, p1, stream=0, dtype=F32):
         _check(lib().bsmr_sddmm_panels(self.h, dA, dB, K, dtype, dP, p0, p1, stream or None),

@@ -18,7 +18,7 @@ constexpr u32 XCD_BUCKETS = 8;      // MI355X XCDs: column bucket -> workgroups 
 struct Plan;
 // fp16/bf16 SDDMM launch (sddmm_half.hip); mode: 1 dense tiles, 2 residual, 3 both
 int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
-                u32 mode, hipStream_t s);
+                u32 mode, hipStream_t s, u32 nb = 1);
 
 u32 block_size_for(u32 M, u32 N, u64 free_mem);
 u32 cluster_block_dim(u32 nbpr);

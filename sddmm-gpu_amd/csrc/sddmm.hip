@@ -53,6 +53,8 @@ struct SddmmArgs {
     const u32* sparseCol;
     u32 diag;  // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long* trace;  // BSMR_DIAG & 32: per-wave {start, mid, end, hw id}; else null
+    // batched launch (grid.y = batch b): A += b * bA, B += b * bB, P += b * bP (elements)
+    unsigned long long bA, bB, bP;
 };
 
 // debug timeline (BSMR_DIAG & 32 only): wave start / mid / end in s_memrealtime ticks (100 MHz)
@@ -333,6 +335,11 @@ __device__ __forceinline__ void residual_panel(const SddmmArgs& a, const uint4 i
 template <int KT, int G>
 __global__ __launch_bounds__(256, (KT >= 256 ? 4 : 8)) void k_sddmm_f32(SddmmArgs a) {
     const unsigned long long t0 = rtime(a.trace);
+    if (blockIdx.y) {
+        a.A += blockIdx.y * a.bA;
+        a.B += blockIdx.y * a.bB;
+        a.P += blockIdx.y * a.bP;
+    }
     const u32 b = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b < a.nd) {
         dense_tile<KT>(a, a.d0 + b);
@@ -402,6 +409,7 @@ struct RbArgs {
     u32 mode;  // 1 = dense tiles, 2 = residual, 3 = both
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
+    unsigned long long bA, bB, bP;  // batched launch, as in SddmmArgs
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -539,6 +547,11 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const float* As,
 template <int KT, int NT>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     extern __shared__ __attribute__((aligned(16))) float As[];
+    if (blockIdx.y) {  // batch b (item -> XCD placement unchanged: nItems is a multiple of 8)
+        a.A += blockIdx.y * a.bA;
+        a.B += blockIdx.y * a.bB;
+        a.P += blockIdx.y * a.bP;
+    }
     constexpr u32 NC = KT / 16;                             // chunks per lane (tile or row-group)
     constexpr u32 NCH = KT / 4;                             // 16-byte chunks per row
     constexpr u32 NW = NT / 64;                             // waves per workgroup
@@ -699,7 +712,7 @@ int ensure_rb_layout(const Plan& p, int slot, u32 K) {
 
 // mode: 1 = dense tiles only, 2 = residual only, 3 = both (profiling splits)
 int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP, u32 mode,
-              hipStream_t s) {
+              hipStream_t s, u32 nb = 1) {
     const Plan::RowBlockLayout& L = p.rbl[slot];
     if (L.nItems == 0) return BSMR_OK;
     RbArgs a{};
@@ -731,19 +744,25 @@ int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP
         default: fn = BSMR_RB(128); break;
     }
 #undef BSMR_RB
-    hipLaunchKernelGGL(fn, dim3(L.nItems), dim3(L.NT), L.lds, s, a);
+    a.bA = static_cast<unsigned long long>(p.M) * L.K;
+    a.bB = static_cast<unsigned long long>(p.N) * L.K;
+    a.bP = p.nnz;
+    hipLaunchKernelGGL(fn, dim3(L.nItems, nb), dim3(L.NT), L.lds, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }
 
-int launch_full(const Plan& p, SddmmArgs a, hipStream_t s) {
+int launch_full(const Plan& p, SddmmArgs a, hipStream_t s, u32 nb = 1) {
     const u32 items = a.nslots ? ((a.nd + 31) & ~31u) + a.nslots : a.nd;
     if (items == 0) return BSMR_OK;
+    a.bA = static_cast<unsigned long long>(p.M) * a.K;
+    a.bB = static_cast<unsigned long long>(p.N) * a.K;
+    a.bP = p.nnz;
     if (p.diag & 32) {
         BSMR_CHECK(p.prepare_trace((items + 3) / 4 * 4, s));
         a.trace = p.trace.data();
     }
-    hipLaunchKernelGGL(pick_kernel<false>(a.K), dim3((items + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pick_kernel<false>(a.K), dim3((items + 3) / 4, nb), dim3(256), 0, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }
@@ -762,24 +781,48 @@ int launch_panels(SddmmArgs a, hipStream_t s) {
 
 using namespace bsmr;
 
-extern "C" int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
-                          int dtype, float* dP, void* stream) {
+// one launch per at most 65535 batches (grid.y); batch b reads A + b*M*K, B + b*N*K and writes
+// P + b*nnz (sddmm_gpu_batch, sddmmKernel.cu:2764-2850)
+extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const void* dA,
+                                const void* dB, uint32_t K, int dtype, float* dP, void* stream) {
     if (!plan) {
         set_error("bsmr_sddmm: null plan");
         return BSMR_ERR_INVALID;
     }
+    if (num_batch == 0) {
+        set_error("bsmr_sddmm_batch: num_batch must be >= 1");
+        return BSMR_ERR_INVALID;
+    }
     const Plan& p = plan->p;
     BSMR_CHECK(validate(dA, dB, K, dtype, dP));
-    if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, 3, static_cast<hipStream_t>(stream));
-    const int slot = rb_slot(p, K);
-    if (slot >= 0) {
-        BSMR_CHECK(ensure_rb_layout(p, slot, K));
-        return launch_rb(p, slot, dA, dB, dP, 3, static_cast<hipStream_t>(stream));
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t es = dtype == BSMR_F32 ? 4 : 2;
+    for (u32 b0 = 0; b0 < num_batch; b0 += 65535u) {
+        const u32 nb = std::min<u32>(num_batch - b0, 65535u);
+        const char* A = static_cast<const char*>(dA) + es * b0 * static_cast<size_t>(p.M) * K;
+        const char* B = static_cast<const char*>(dB) + es * b0 * static_cast<size_t>(p.N) * K;
+        float* P = dP + static_cast<size_t>(b0) * p.nnz;
+        if (dtype != BSMR_F32) {
+            BSMR_CHECK(launch_half(p, A, B, K, dtype, P, 3, s, nb));
+            continue;
+        }
+        const int slot = rb_slot(p, K);
+        if (slot >= 0) {
+            BSMR_CHECK(ensure_rb_layout(p, slot, K));
+            BSMR_CHECK(launch_rb(p, slot, A, B, P, 3, s, nb));
+            continue;
+        }
+        SddmmArgs a = make_args(p, A, B, K, P);
+        a.nd = p.nDenseItems;
+        a.nslots = p.nSlots;
+        BSMR_CHECK(launch_full(p, a, s, nb));
     }
-    SddmmArgs a = make_args(p, dA, dB, K, dP);
-    a.nd = p.nDenseItems;
-    a.nslots = p.nSlots;
-    return launch_full(p, a, static_cast<hipStream_t>(stream));
+    return BSMR_OK;
+}
+
+extern "C" int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
+                          int dtype, float* dP, void* stream) {
+    return bsmr_sddmm_batch(plan, 1, dA, dB, K, dtype, dP, stream);
 }
 
 extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const void* dB,

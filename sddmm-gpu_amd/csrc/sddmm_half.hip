@@ -32,6 +32,7 @@ struct HalfArgs {
     const u32* cmCol;
     const u32* cmOut;
     u32 N, K;
+    unsigned long long bA, bB, bP;  // batched launch (grid.y = batch), element strides
 };
 
 template <bool BF16>
@@ -144,6 +145,11 @@ __device__ __forceinline__ void residual_h(const HalfArgs& a, const uint2 sl) {
 
 template <bool BF16>
 __global__ __launch_bounds__(64) void k_sddmm_half(HalfArgs a) {
+    if (blockIdx.y) {
+        a.A += blockIdx.y * a.bA;
+        a.B += blockIdx.y * a.bB;
+        a.P += blockIdx.y * a.bP;
+    }
     const u32 b = blockIdx.x;
     if (b < a.nd) {
         dense_tile_h<BF16>(a, b);
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(64) void k_sddmm_half(HalfArgs a) {
 
 // dtype: BSMR_F16 or BSMR_BF16; K a positive multiple of 32. mode: 1 dense, 2 residual, 3 both
 int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
-                u32 mode, hipStream_t s) {
+                u32 mode, hipStream_t s, u32 nb) {
     if (K == 0 || K % 32 != 0) {
         set_error("bsmr_sddmm: fp16/bf16 inputs need K to be a positive multiple of 32");
         return BSMR_ERR_UNSUPPORTED;
@@ -182,12 +188,15 @@ int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype,
     a.cmOut = p.cmOut.data();
     a.N = p.N;
     a.K = K;
+    a.bA = static_cast<unsigned long long>(p.M) * K;
+    a.bB = static_cast<unsigned long long>(p.N) * K;
+    a.bP = p.nnz;
     const u32 grid = a.nslots ? ((a.nd + 7) & ~7u) + a.nslots : a.nd;
     if (grid == 0) return BSMR_OK;
     if (dtype == BSMR_BF16)
-        hipLaunchKernelGGL(k_sddmm_half<true>, dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_sddmm_half<true>, dim3(grid, nb), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL(k_sddmm_half<false>, dim3(grid), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_sddmm_half<false>, dim3(grid, nb), dim3(64), 0, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }

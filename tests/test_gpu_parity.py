@@ -14,7 +14,7 @@ import oracle_lib as O
 from bsmr import Plan, make_data, synth
 from golden_common import (ALPHAS, DELTAS, REF_FREE_MEM, compare, expected_from_stats, matrix,
                            record)
-from gpu_util import assert_plans_equal, oracle_plan, run_sddmm
+from gpu_util import assert_plans_equal, oracle_plan, run_sddmm, torch_cuda
 
 pytestmark = pytest.mark.gpu
 
@@ -198,3 +198,25 @@ def test_values_independent_of_layout_permutation():
         plan = Plan(M, N, rp, ci, alpha=alpha, delta=delta, free_mem_bytes=FREE)
         P = run_sddmm(plan, A, B, K, len(ci))
         assert O.check_data(ref, P) == 0
+
+
+@pytest.mark.parametrize("K,layout,nb", [(128, "auto", 3), (64, "colmajor", 2), (96, "auto", 4)])
+def test_sddmm_batch_each_batch_checkdata(K, layout, nb):
+    """sddmm_gpu_batch semantics: batch b = (A_b, B_b) at strides M*K / N*K, P_b at b*nnz."""
+    torch = torch_cuda()
+    M, N, rp, ci = small_cases()["zipf"]
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout=layout)
+    A = make_data(nb * M * K)
+    B = make_data(nb * N * K)[::-1].copy()  # different values per batch
+    dA = torch.from_numpy(A).cuda()
+    dB = torch.from_numpy(B).cuda()
+    nnz = len(ci)
+    dP = torch.full((nb * nnz,), float("nan"), dtype=torch.float32, device="cuda")
+    plan.sddmm_batch(nb, dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+                     stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    P = dP.cpu().numpy()
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    for b in range(nb):
+        ref = O.sddmm_cpu(c, K, A[b * M * K:(b + 1) * M * K], B[b * N * K:(b + 1) * N * K])
+        assert O.check_data(ref, P[b * nnz:(b + 1) * nnz]) == 0, b
