@@ -232,8 +232,10 @@ def main():
             dist.destroy_process_group()
         return
     # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
-    if dtype == F32 and K in (64, 128):
-        kern = f"k_sddmm_rb<{K},1024> (row-block LDS layout: dense-tile MFMA + residual)"
+    rby = K * (4 if dtype == F32 else 2)
+    if rby in (256, 512):
+        kern = (f"k_sddmm_rb<{dtype},{rby},1024> (row-block LDS layout, {rby}-byte rows: "
+                "dense-tile MFMA + residual)")
     elif dtype == F32:
         kern = f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)"
     else:

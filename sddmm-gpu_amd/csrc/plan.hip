@@ -807,10 +807,10 @@ u32 kept_warp_mask(u32 B) {
     return reach[0];
 }
 
-// Rows per row block for a K: a multiple of 16 with RB * K * 4 bytes within the LDS budget, at
-// most 1024 (10-bit local row in the entry metadata) and no more than the matrix needs.
-u32 rowblock_rows(u32 K, u32 lds_kb, u32 R) {
-    u32 rb = static_cast<u32>(static_cast<u64>(lds_kb) * 1024 / (4ull * K) / 16 * 16);
+// Rows per row block for rows of rowBytes: a multiple of 16 with RB * rowBytes within the LDS
+// budget, at most 1024 (10-bit local row in the entry metadata) and no more than the matrix needs.
+u32 rowblock_rows(u32 rowBytes, u32 lds_kb, u32 R) {
+    u32 rb = static_cast<u32>(static_cast<u64>(lds_kb) * 1024 / rowBytes / 16 * 16);
     rb = std::min<u32>(std::max<u32>(rb, 16), 1024);
     return std::min<u32>(rb, std::max<u32>((R + 15) / 16 * 16, 16));
 }
@@ -839,18 +839,17 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
 }
 }  // namespace
 
-int Plan::build_rowblock_layout(int slot, u32 K) const {
+int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
     RowBlockLayout& L = rbl[slot];
-    L.K = 0;
+    L.rowBytes = 0;
     hipStream_t s = stream;
     if (N > (1u << 22)) {
         set_error("row-block layout needs N <= 2^22");
         return BSMR_ERR_UNSUPPORTED;
     }
-    const u32 KS = std::min<u32>(K, 128);  // k-slice staged in LDS (sddmm.hip)
-    const u32 RBr = rowblock_rows(KS, rb_lds_kb, R);
+    const u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, R);
     const u32 nRB = (R + RBr - 1) / RBr;
-    const size_t lds = static_cast<size_t>(RBr) * KS * sizeof(float);
+    const size_t lds = static_cast<size_t>(RBr) * rowBytes;
     const u32 NT = lds > 80 * 1024 ? 1024 : 512;
     const u32 wgPerCU = std::max<u32>(1, std::min<u32>(static_cast<u32>(160 * 1024 / lds), 2048 / NT));
     int cus = 256;
@@ -922,31 +921,65 @@ int Plan::build_rowblock_layout(int slot, u32 K) const {
             cost[i] = (se1[i] - se0[i]) + 16.0 * (st1[i] - st0[i]);
         }
     }
-    // chunks per bucket: one round of workgroup slots unless items would drop below ~512 units
+    // chunks: one round of workgroup slots (Q items) unless items would drop below ~512 units. A
+    // row block big enough for >= 8 items is split by the XCD column ranges (its items then read B
+    // from their own XCD's L2); a smaller one (e.g. banded matrices: many row blocks of few
+    // entries) is cut along its whole column-sorted entry list, and its items go to the list with
+    // the fewest items. Item counts come from largest-remainder apportionment, so one round of
+    // slots is not exceeded unless there are more row blocks than slots.
     std::vector<std::vector<uint4>> lists(XCD_BUCKETS);
     std::vector<std::vector<u32>> lends(XCD_BUCKETS);
-    const double minItem = 512.0;
+    double total = 0;
+    for (double c : cost) total += c;
+    const u32 Q = std::max<u32>(1, std::min<u32>(perBucket * XCD_BUCKETS, static_cast<u32>(total / 512.0)));
+    const double target = total / Q;
+    std::vector<double> cb(nRB, 0.0);
+    std::vector<char> split(nRB, 0);
+    double splitTotal = 0;
+    for (u32 b = 0; b < nRB; ++b) {
+        for (u32 x = 0; x < XCD_BUCKETS; ++x) cb[b] += cost[b * XCD_BUCKETS + x];
+        split[b] = cb[b] >= XCD_BUCKETS * target;
+        if (split[b]) splitTotal += cb[b];
+    }
+    // the same quota for every bucket (the column cuts balance them): an extra item in one
+    // bucket would start a second round of slots on that XCD
+    const u32 qEach = static_cast<u32>(
+        std::llround(static_cast<double>(Q / XCD_BUCKETS) * (total > 0 ? splitTotal / total : 0.0)));
+    const u32 qSplit = qEach * XCD_BUCKETS;
+    const std::vector<u32> qx(XCD_BUCKETS, qEach);
+    std::vector<double> cu(nRB, 0.0);
+    for (u32 b = 0; b < nRB; ++b) cu[b] = split[b] ? 0.0 : cb[b];
+    const std::vector<u32> nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u);
+    auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch) {
+        for (u32 k = 0; k < nch; ++k) {
+            const u32 ea = e0 + static_cast<u32>(static_cast<u64>(ne) * k / nch);
+            const u32 eb = e0 + static_cast<u32>(static_cast<u64>(ne) * (k + 1) / nch);
+            const u32 ta = t0 + static_cast<u32>(static_cast<u64>(nt) * k / nch);
+            const u32 tb = t0 + static_cast<u32>(static_cast<u64>(nt) * (k + 1) / nch);
+            if (ea == eb && ta == tb) continue;
+            u32 to = xl;
+            if (to >= XCD_BUCKETS) {  // unsplit: the list with the fewest items
+                to = 0;
+                for (u32 y = 1; y < XCD_BUCKETS; ++y)
+                    if (lists[y].size() < lists[to].size()) to = y;
+            }
+            lists[to].push_back(make_uint4(b, ta, tb, ea));
+            lends[to].push_back(eb);
+        }
+    };
     for (u32 x = 0; x < XCD_BUCKETS; ++x) {
-        std::vector<double> cx(nRB);
-        double tx = 0;
-        for (u32 b = 0; b < nRB; ++b) tx += (cx[b] = cost[b * XCD_BUCKETS + x]);
-        if (tx <= 0) continue;
-        const u32 rounds = std::max<u32>(1, static_cast<u32>(std::ceil(tx / (perBucket * 65536.0))));
-        const u32 q = std::max<u32>(1, std::min<u32>(perBucket * rounds, static_cast<u32>(tx / minItem)));
-        const std::vector<u32> nch = apportion(cx, q);
+        std::vector<double> c(nRB, 0.0);
+        for (u32 b = 0; b < nRB; ++b) c[b] = split[b] ? cost[b * XCD_BUCKETS + x] : 0.0;
+        const std::vector<u32> nch = apportion(c, qx[x]);
         for (u32 b = 0; b < nRB; ++b) {
             const u32 i = b * XCD_BUCKETS + x;
-            const u32 ne = se1[i] - se0[i], nt = st1[i] - st0[i];
-            for (u32 c = 0; c < nch[b]; ++c) {
-                const u32 ea = se0[i] + static_cast<u32>(static_cast<u64>(ne) * c / nch[b]);
-                const u32 eb = se0[i] + static_cast<u32>(static_cast<u64>(ne) * (c + 1) / nch[b]);
-                const u32 ta = st0[i] + static_cast<u32>(static_cast<u64>(nt) * c / nch[b]);
-                const u32 tb = st0[i] + static_cast<u32>(static_cast<u64>(nt) * (c + 1) / nch[b]);
-                if (ea == eb && ta == tb) continue;
-                lists[x].push_back(make_uint4(b, ta, tb, ea));
-                lends[x].push_back(eb);
-            }
+            if (nch[b]) emit(x, b, se0[i], se1[i] - se0[i], st0[i], st1[i] - st0[i], nch[b]);
         }
+    }
+    for (u32 b = 0; b < nRB; ++b) {
+        if (!nu[b]) continue;
+        const u32 i0 = b * XCD_BUCKETS, i1 = i0 + XCD_BUCKETS - 1;
+        emit(XCD_BUCKETS, b, se0[i0], se1[i1] - se0[i0], st0[i0], st1[i1] - st0[i0], nu[b]);
     }
     size_t nmax = 0;
     for (const auto& l : lists) nmax = std::max(nmax, l.size());
@@ -989,7 +1022,7 @@ int Plan::build_rowblock_layout(int slot, u32 K) const {
     L.NT = NT;
     L.lds = lds;
     L.nRB = nRB;
-    L.K = K;
+    L.rowBytes = rowBytes;
     return BSMR_OK;
 }
 
@@ -1160,7 +1193,7 @@ int Plan::build_columns() {
             s));
         segments_ready = true;
     }
-    for (auto& L : rbl) L.K = 0;  // K-specific launch layouts depend on the column split
+    for (auto& L : rbl) L.rowBytes = 0;  // launch layouts depend on the column split
     // pass 1
     const u32 thr =static_cast<u32>(std::ceil(delta * static_cast<float>(TILE)));  // colReordering.cu:246
     DevBuf<u32> phist, pnd, pns, psd;

@@ -78,7 +78,7 @@ struct Plan {
     // 4-lane row-groups of a workgroup take one piece each per phase, so every group loads its B
     // column in the same (full-width) instruction. items[i].w / itemEnd[i] delimit its pieces.
     struct RowBlockLayout {
-        u32 K = 0, RB = 0, NT = 1024, nRB = 0, nItems = 0, nPieces = 0;
+        u32 rowBytes = 0, RB = 0, NT = 1024, nRB = 0, nItems = 0, nPieces = 0;
         size_t lds = 0;
         DevBuf<u32> meta;   // local row << 22 | column
         DevBuf<u32> out;    // output index (CSR position)
@@ -86,9 +86,9 @@ struct Plan {
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}
     };
-    static constexpr int N_RB_LAYOUTS = 4;  // K = 64, 128, 256, 512
+    static constexpr int N_RB_LAYOUTS = 2;  // rows of 256 and 512 bytes
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
-    int build_rowblock_layout(int slot, u32 K) const;
+    int build_rowblock_layout(int slot, u32 rowBytes) const;
 
     mutable DevBuf<uint8_t> tmp;  // scan/sort scratch
     // BSMR_DIAG & 32 debug timeline (4 u64 per wave of the last launch)

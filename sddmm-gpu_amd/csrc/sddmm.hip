@@ -374,18 +374,18 @@ __global__ __launch_bounds__(64) void k_sddmm_panels_f32(SddmmArgs a) {
 }
 
 // ==========================================================================================
-// Row-block launch (K = 64, 128): one workgroup per item {row block rb, tiles [t0, t1), residual
-// entries [e0, e1)} (layout: Plan::build_rowblock_layout). The A rows of the RB reordered
-// positions of rb are staged in LDS once (<= 144 KiB); dense tiles take their MFMA A operand and
-// residual entries their A pieces from LDS, so the only gathered operand is B, read once per
-// column run (entries are sorted by (row block, column)), from the L2 of the XCD that owns the
-// item's column range.
+// Row-block launch (rows of RBY = 256 or 512 bytes: fp32 K = 64/128, fp16/bf16 K = 128/256): one
+// workgroup per item {row block rb, tiles [t0, t1), residual pieces [p0, p1)} (layout:
+// Plan::build_rowblock_layout). The A rows of the RB reordered positions of rb are staged in LDS
+// once (<= 144 KiB); dense tiles take their MFMA A operand and residual entries their A pieces
+// from LDS, so the only gathered operand is B, read once per column run (entries are sorted by
+// (row block, column)).
 //
 // Residual entries: G = 4 lanes per entry (16 row-groups per wave), so the per-entry bookkeeping
-// (metadata broadcast, addresses, column-change test, store) is shared by 16 entries per wave
-// instruction; each lane owns NC = K/16 chunks (16 B) 4t + s of the row, multiplies them with
-// packed FMAs and the quad reduces with two DPP adds.
-// LDS image: row lr at lr * K floats (unpadded); chunk c of row lr sits at
+// (metadata broadcast, addresses, store) is shared by 16 entries per wave instruction; each lane
+// owns NC = RBY/64 16-byte chunks 4t + s of the row (packed FMA for fp32, v_dot2 for fp16/bf16,
+// fp32 accumulation) and the quad reduces with two DPP adds.
+// LDS image: row lr at lr * RBY bytes (unpadded); chunk c of row lr sits at
 // (c & ~3) | ((c & 3) ^ (lr & 3)). Lane (row-group j, sub s) visits its chunks in the rotated
 // order t = (f + j) mod NC, so in every ds_read_b128 lane group ({0-3,12-15,20-27},
 // {4-11,16-19,28-31}, +32 = row-groups {0,3,5,6}, {1,2,4,7}, ...) the four row-groups read four
@@ -393,8 +393,8 @@ __global__ __launch_bounds__(64) void k_sddmm_panels_f32(SddmmArgs a) {
 // Dense tiles read chunk 16w + 4g + j of the 16 tile rows: the XOR spreads rows 0-3 (2-way).
 // ==========================================================================================
 struct RbArgs {
-    const float* A;
-    const float* B;
+    const char* A;  // row-major M x K elements of the dtype
+    const char* B;  // N rows of K elements (B column-major)
     float* P;
     const u32* rows;
     u32 R, N, RB;
@@ -409,12 +409,18 @@ struct RbArgs {
     u32 mode;  // 1 = dense tiles, 2 = residual, 3 = both
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
-    unsigned long long bA, bB, bP;  // batched launch, as in SddmmArgs
+    unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ u32 lds_chunk(u32 lr, u32 c) { return (c & ~3u) | ((c & 3u) ^ (lr & 3u)); }
+
+__device__ __forceinline__ f32x4 ld16(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 // value of lane I of the quad in every lane of the quad
 template <int I>
@@ -423,12 +429,54 @@ __device__ __forceinline__ u32 quad_bcast(u32 v) {
         __builtin_amdgcn_update_dpp(0, static_cast<int>(v), I * 0x55, 0xF, 0xF, false));
 }
 
+// acc += a . b over one 16-byte chunk (DT 0: 4 fp32, packed FMA; 1: 8 fp16, 2: 8 bf16, v_dot2)
+template <int DT>
+__device__ __forceinline__ void chunk_dot(const f32x4 a, const f32x4 b, f32x2& acc0, f32x2& acc1) {
+    if constexpr (DT == 0) {
+        acc0 = __builtin_elementwise_fma(f32x2{a.x, a.y}, f32x2{b.x, b.y}, acc0);
+        acc1 = __builtin_elementwise_fma(f32x2{a.z, a.w}, f32x2{b.z, b.w}, acc1);
+    } else if constexpr (DT == 1) {
+        // whole-vector bit casts + swizzles: __builtin_bit_cast of a vector ELEMENT miscompiles
+        // here (hipcc 7.2 reads element 0 for every index)
+        const h16x8 ha = __builtin_bit_cast(h16x8, a), hb = __builtin_bit_cast(h16x8, b);
+        acc0.x = __builtin_amdgcn_fdot2(ha.s01, hb.s01, acc0.x, false);
+        acc0.y = __builtin_amdgcn_fdot2(ha.s23, hb.s23, acc0.y, false);
+        acc1.x = __builtin_amdgcn_fdot2(ha.s45, hb.s45, acc1.x, false);
+        acc1.y = __builtin_amdgcn_fdot2(ha.s67, hb.s67, acc1.y, false);
+    } else {
+        const b16x8 ha = __builtin_bit_cast(b16x8, a), hb = __builtin_bit_cast(b16x8, b);
+        acc0.x = __builtin_amdgcn_fdot2_f32_bf16(ha.s01, hb.s01, acc0.x, false);
+        acc0.y = __builtin_amdgcn_fdot2_f32_bf16(ha.s23, hb.s23, acc0.y, false);
+        acc1.x = __builtin_amdgcn_fdot2_f32_bf16(ha.s45, hb.s45, acc1.x, false);
+        acc1.y = __builtin_amdgcn_fdot2_f32_bf16(ha.s67, hb.s67, acc1.y, false);
+    }
+}
+
+// acc += the MFMA of one 16-byte A chunk and B chunk per lane (DT 0: four 16x16x4 f32 steps;
+// 1/2: one 16x16x32 f16/bf16 step), lane layout of dense_tile (one k-block per lane group)
+template <int DT>
+__device__ __forceinline__ f32x4 chunk_mfma(const f32x4 a, const f32x4 b, f32x4 acc) {
+    if constexpr (DT == 0) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+    } else if constexpr (DT == 1) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h16x8, a),
+                                                      __builtin_bit_cast(h16x8, b), acc, 0, 0, 0);
+    } else {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8, a),
+                                                       __builtin_bit_cast(b16x8, b), acc, 0, 0, 0);
+    }
+}
+
 // dense tile on the LDS image: load() gathers the tile's metadata and B operand (no LDS, so a
 // wave can issue it before the staging barrier), run() reads the A rows from LDS, runs the MFMAs
-// and scatters the 256 outputs
-template <int KT>
+// and scatters the 256 outputs. Lane group g takes chunk 16w + 4g + j at k-step 4w + j (any
+// k-permutation shared by A and B is valid), so the XOR of the LDS image spreads it.
+template <int DT, int RBY>
 struct DenseTileLds {
-    static constexpr int NK = KT / 16;  // k-steps; step kk = 4w + j covers chunks 16w + 4g + j
+    static constexpr int NK = RBY / 64;  // 16-byte chunks per lane
     u32 lr, idx[4];
     __device__ __forceinline__ static u32 chunk(int kk, u32 g) {
         return 16 * (kk >> 2) + 4 * g + (kk & 3);
@@ -443,22 +491,19 @@ struct DenseTileLds {
         for (int r = 0; r < 4; ++r) idx[r] = bvals[16 * r];
         lr = p * 16 - q0 + rr;
         const bool cvalid = c < a.N;
-        const float* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * KT;
+        const char* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * RBY;
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) bv[kk] = cvalid ? ld4(bcol + 4 * chunk(kk, g)) : f32x4{0, 0, 0, 0};
+        for (int kk = 0; kk < NK; ++kk) bv[kk] = cvalid ? ld16(bcol + 16 * chunk(kk, g)) : f32x4{0, 0, 0, 0};
     }
-    __device__ __forceinline__ void run(const RbArgs& a, const float* As, const f32x4 (&bv)[NK]) const {
+    __device__ __forceinline__ void run(const RbArgs& a, const char* As, const f32x4 (&bv)[NK]) const {
         const u32 g = __lane_id() >> 4;
-        const float* arow = As + lr * KT;
+        const char* arow = As + lr * RBY;
         f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) {
-            const f32x4 av = *reinterpret_cast<const f32x4*>(arow + 4 * lds_chunk(lr, chunk(kk, g)));
+            const f32x4 av = ld16(arow + 16 * lds_chunk(lr, chunk(kk, g)));
             f32x4& acc = (kk & 1) ? acc1 : acc0;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[kk].x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[kk].y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[kk].z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[kk].w, acc, 0, 0, 0);
+            acc = chunk_mfma<DT>(av, bv[kk], acc);
         }
         const f32x4 acc = acc0 + acc1;
 #pragma unroll
@@ -468,13 +513,12 @@ struct DenseTileLds {
 };
 
 // B pieces of the group's column (lane s: chunks 4 * ((f + j) mod NC) + s, f < NC)
-template <int KT>
+template <int RBY>
 __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const u32 sub,
-                                          const u32 (&rot)[KT / 16], f32x4 (&bv)[KT / 16]) {
-    const char* Bb = reinterpret_cast<const char*>(a.B);
-    const u32 bb = col * (KT * 4) + 16 * sub;
+                                          const u32 (&rot)[RBY / 64], f32x4 (&bv)[RBY / 64]) {
+    const u32 bb = col * RBY + 16 * sub;
 #pragma unroll
-    for (u32 f = 0; f < KT / 16; ++f) bv[f] = *reinterpret_cast<const f32x4*>(Bb + (bb + rot[f]));
+    for (u32 f = 0; f < RBY / 64; ++f) bv[f] = ld16(a.B + (bb + rot[f]));
 }
 
 // a column-run piece of a row-group: entries [first, first + len), len <= RB_PIECE_MAX = 16, all
@@ -484,14 +528,14 @@ struct Piece {
     u32 mm[4], mo[4];
 };
 
-template <int KT>
+template <int RBY>
 __device__ __forceinline__ void load_piece(const RbArgs& a, const u32 pi, const u32 sub,
-                                           const u32 (&rot)[KT / 16], f32x4 (&bv)[KT / 16],
+                                           const u32 (&rot)[RBY / 64], f32x4 (&bv)[RBY / 64],
                                            Piece& pc) {
     const uint2 d = a.pieces[pi];
     pc.first = d.x;
     pc.len = (d.y >> 22) + 1;
-    load_bcol<KT>(a, d.y & 0x3FFFFFu, sub, rot, bv);
+    load_bcol<RBY>(a, d.y & 0x3FFFFFu, sub, rot, bv);
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         const u32 e = 4 * k + sub;
@@ -502,12 +546,11 @@ __device__ __forceinline__ void load_piece(const RbArgs& a, const u32 pi, const 
 
 // Step i of a batch of 4 computes entry 4k + i in all 4 lanes; lane i keeps it, so a batch ends
 // in one store instruction for 4 entries per group (64 outputs per full wave).
-template <int KT>
-__device__ __forceinline__ void residual_piece(const RbArgs& a, const float* As, const Piece& pc,
-                                               const u32 sub, const u32 (&rot)[KT / 16],
-                                               const f32x4 (&bv)[KT / 16]) {
-    constexpr u32 NC = KT / 16;
-    const char* Ab = reinterpret_cast<const char*>(As);
+template <int DT, int RBY>
+__device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As, const Piece& pc,
+                                               const u32 sub, const u32 (&rot)[RBY / 64],
+                                               const f32x4 (&bv)[RBY / 64]) {
+    constexpr u32 NC = RBY / 64;
 #pragma unroll
     for (u32 k = 0; k < 4; ++k) {
         if (4 * k >= pc.len) break;
@@ -524,16 +567,13 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const float* As,
                 default: m = quad_bcast<3>(pc.mm[k]); break;
             }
             const u32 lr = m >> 22;
-            const u32 ab = lr * (KT * 4) + 16 * (sub ^ (lr & 3));
+            const u32 ab = lr * RBY + 16 * (sub ^ (lr & 3));
             f32x4 av[NC];  // all NC reads in flight before the first FMA
 #pragma unroll
-            for (u32 f = 0; f < NC; ++f) av[f] = *reinterpret_cast<const f32x4*>(Ab + (ab + rot[f]));
+            for (u32 f = 0; f < NC; ++f) av[f] = ld16(As + (ab + rot[f]));
             f32x2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
 #pragma unroll
-            for (u32 f = 0; f < NC; ++f) {
-                acc0 = __builtin_elementwise_fma(f32x2{av[f].x, av[f].y}, f32x2{bv[f].x, bv[f].y}, acc0);
-                acc1 = __builtin_elementwise_fma(f32x2{av[f].z, av[f].w}, f32x2{bv[f].z, bv[f].w}, acc1);
-            }
+            for (u32 f = 0; f < NC; ++f) chunk_dot<DT>(av[f], bv[f], acc0, acc1);
             const f32x2 acc = acc0 + acc1;
             float sm = acc.x + acc.y;
             sm += dppf<0xB1>(sm);  // quad_perm [1,0,3,2]
@@ -544,17 +584,18 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const float* As,
     }
 }
 
-template <int KT, int NT>
+template <int DT, int RBY, int NT>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float As[];
+    extern __shared__ __attribute__((aligned(16))) char AsB[];
+    char* As = AsB;
     if (blockIdx.y) {  // batch b (item -> XCD placement unchanged: nItems is a multiple of 8)
         a.A += blockIdx.y * a.bA;
         a.B += blockIdx.y * a.bB;
         a.P += blockIdx.y * a.bP;
     }
-    constexpr u32 NC = KT / 16;                             // chunks per lane (tile or row-group)
-    constexpr u32 NCH = KT / 4;                             // 16-byte chunks per row
-    constexpr u32 NW = NT / 64;                             // waves per workgroup
+    constexpr u32 NC = RBY / 64;  // chunks per lane (tile or row-group)
+    constexpr u32 NW = NT / 64;   // waves per workgroup
+    constexpr u32 NG = NT / 4;    // residual row-groups
     const unsigned long long t0 = rtime(a.trace);
     const uint4 it = a.items[blockIdx.x];
     const u32 pend = a.itemEnd[blockIdx.x];
@@ -566,24 +607,23 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // staging loads so all of it is in flight together
     const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
     const u32 np = (a.mode & 2) ? pend - it.w : 0u;
-    constexpr u32 NG = NT / 4;  // residual row-groups
     const u32 gr = tid >> 2;
     u32 rot[NC];  // residual: byte offset of the 64-byte quad the lane visits at step f
 #pragma unroll
     for (u32 f = 0; f < NC; ++f) rot[f] = 64u * ((f + j) % NC);
     f32x4 tb[NC], pre[NC];
-    DenseTileLds<KT> dt;
+    DenseTileLds<DT, RBY> dt;
     // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
     const u32 tw = NW - 1 - w;
     if (tw < ntile) dt.load(a, it.y + tw, q0, tb);
     Piece pc;
     pc.len = 0;
-    if (gr < np) load_piece<KT>(a, it.w + gr, sub, rot, pre, pc);
+    if (gr < np) load_piece<RBY>(a, it.w + gr, sub, rot, pre, pc);
     // stage the row block by LDS-DMA: each wave-instruction fills one contiguous KiB of the image
     // (RPB rows); lane l supplies row lr = RPB * b + l / LPR at physical chunk pc = l % LPR, read
     // from the logical chunk lds_chunk(lr, pc) of A[rows[q0 + lr]] (the XOR is an involution)
     {
-        constexpr u32 LPR = KT / 4, RPB = 64 / LPR;
+        constexpr u32 LPR = RBY / 16, RPB = 64 / LPR;
         // KiB blocks per wave (max): NT = 512 is launched only for images <= 80 KiB
         constexpr u32 MAXB = ((NT == 1024 ? 160u : 80u) + NW - 1) / NW;
         const u32 lane = tid & 63, nblk = a.RB / RPB;
@@ -597,9 +637,9 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         for (u32 i = 0; i < MAXB; ++i) {
             const u32 b = w + i * NW, lr = b * RPB + lane / LPR;
             if (b < nblk) {
-                const float* g = a.A + static_cast<size_t>(src[i]) * KT + 4 * lds_chunk(lr, lane % LPR);
+                const char* g = a.A + static_cast<size_t>(src[i]) * RBY + 16 * lds_chunk(lr, lane % LPR);
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                                 (__attribute__((address_space(3))) void*)(As + 256 * b),
+                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
                                                  16, 0, 0);
             }
         }
@@ -612,14 +652,14 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     }
     if (tw < ntile) dt.run(a, As, tb);
     const unsigned long long td = rtime(a.trace);
-    if (pc.len) residual_piece<KT>(a, As, pc, sub, rot, pre);
+    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     // later phases (items with more pieces than row-groups): the extra pieces are the shortest
     // and go to the groups that had the shortest phase-0 pieces
     for (u32 ph = 1; ph * NG < np; ++ph) {
         const u32 pi = ph * NG + (NG - 1 - gr);
         if (pi < np) {
-            load_piece<KT>(a, it.w + pi, sub, rot, pre, pc);
-            residual_piece<KT>(a, As, pc, sub, rot, pre);
+            load_piece<RBY>(a, it.w + pi, sub, rot, pre, pc);
+            residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
         }
     }
     for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
@@ -694,30 +734,28 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
     return a;
 }
 
-// K -> row-block layout slot (-1: use the column-major path)
-int rb_slot(const Plan& p, u32 K) {
+// (K, dtype) -> row-block layout slot by row bytes (0: 256 B, 1: 512 B); -1: column-major path
+int rb_slot(const Plan& p, u32 K, int dtype) {
     if (p.N > (1u << 22) || !p.use_rowblock) return -1;
-    switch (K) {
-        case 64: return 0;
-        case 128: return 1;
-        default: return -1;
-    }
+    if (dtype == BSMR_F32) return K == 64 ? 0 : K == 128 ? 1 : -1;
+    return K == 128 ? 0 : K == 256 ? 1 : -1;
 }
 
-int ensure_rb_layout(const Plan& p, int slot, u32 K) {
+int ensure_rb_layout(const Plan& p, int slot) {
     std::lock_guard<std::mutex> g(p.layout_mu);
-    if (p.rbl[slot].K == K) return BSMR_OK;
-    return p.build_rowblock_layout(slot, K);
+    const u32 rby = slot == 0 ? 256 : 512;
+    if (p.rbl[slot].rowBytes == rby) return BSMR_OK;
+    return p.build_rowblock_layout(slot, rby);
 }
 
 // mode: 1 = dense tiles only, 2 = residual only, 3 = both (profiling splits)
-int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP, u32 mode,
-              hipStream_t s, u32 nb = 1) {
+int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP, int dtype,
+              u32 mode, hipStream_t s, u32 nb = 1) {
     const Plan::RowBlockLayout& L = p.rbl[slot];
     if (L.nItems == 0) return BSMR_OK;
     RbArgs a{};
-    a.A = static_cast<const float*>(dA);
-    a.B = static_cast<const float*>(dB);
+    a.A = static_cast<const char*>(dA);
+    a.B = static_cast<const char*>(dB);
     a.P = dP;
     a.rows = p.rows.data();
     a.R = p.R;
@@ -737,16 +775,19 @@ int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP
         BSMR_CHECK(p.prepare_trace(static_cast<size_t>(L.nItems) * (L.NT / 64), s));
         a.trace = p.trace.data();
     }
-    void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(KT) (L.NT == 1024 ? k_sddmm_rb<KT, 1024> : k_sddmm_rb<KT, 512>)
-    switch (L.K) {
-        case 64: fn = BSMR_RB(64); break;
-        default: fn = BSMR_RB(128); break;
-    }
-#undef BSMR_RB
-    a.bA = static_cast<unsigned long long>(p.M) * L.K;
-    a.bB = static_cast<unsigned long long>(p.N) * L.K;
+    a.bA = static_cast<unsigned long long>(p.M) * L.rowBytes;
+    a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
+    void (*fn)(RbArgs) = nullptr;
+#define BSMR_RB(DT, RBY) (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>)
+#define BSMR_RB2(DT) (L.rowBytes == 256 ? BSMR_RB(DT, 256) : BSMR_RB(DT, 512))
+    switch (dtype) {
+        case BSMR_F32: fn = BSMR_RB2(0); break;
+        case BSMR_F16: fn = BSMR_RB2(1); break;
+        default: fn = BSMR_RB2(2); break;
+    }
+#undef BSMR_RB2
+#undef BSMR_RB
     hipLaunchKernelGGL(fn, dim3(L.nItems, nb), dim3(L.NT), L.lds, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
@@ -802,14 +843,14 @@ extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const
         const char* A = static_cast<const char*>(dA) + es * b0 * static_cast<size_t>(p.M) * K;
         const char* B = static_cast<const char*>(dB) + es * b0 * static_cast<size_t>(p.N) * K;
         float* P = dP + static_cast<size_t>(b0) * p.nnz;
-        if (dtype != BSMR_F32) {
-            BSMR_CHECK(launch_half(p, A, B, K, dtype, P, 3, s, nb));
+        const int slot = rb_slot(p, K, dtype);
+        if (slot >= 0) {
+            BSMR_CHECK(ensure_rb_layout(p, slot));
+            BSMR_CHECK(launch_rb(p, slot, A, B, P, dtype, 3, s, nb));
             continue;
         }
-        const int slot = rb_slot(p, K);
-        if (slot >= 0) {
-            BSMR_CHECK(ensure_rb_layout(p, slot, K));
-            BSMR_CHECK(launch_rb(p, slot, A, B, P, 3, s, nb));
+        if (dtype != BSMR_F32) {
+            BSMR_CHECK(launch_half(p, A, B, K, dtype, P, 3, s, nb));
             continue;
         }
         SddmmArgs a = make_args(p, A, B, K, P);
@@ -877,8 +918,8 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipEvent_t ev[4];
     for (auto& e : ev) BSMR_HIP(hipEventCreate(&e));
-    const int slot = rb_slot(p, K);
-    if (slot >= 0) BSMR_CHECK(ensure_rb_layout(p, slot, K));
+    const int slot = rb_slot(p, K, dtype);
+    if (slot >= 0) BSMR_CHECK(ensure_rb_layout(p, slot));
     SddmmArgs full = make_args(p, dA, dB, K, dP);
     full.nd = p.nDenseItems;
     full.nslots = p.nSlots;
@@ -887,8 +928,8 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     SddmmArgs res = full;
     res.nd = 0;
     auto run = [&](u32 mode) -> int {
+        if (slot >= 0) return launch_rb(p, slot, dA, dB, dP, dtype, mode, s);
         if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, mode, s);
-        if (slot >= 0) return launch_rb(p, slot, dA, dB, dP, mode, s);
         return launch_full(p, mode == 1 ? dense : mode == 2 ? res : full, s);
     };
     BSMR_HIP(hipEventRecord(ev[0], s));

@@ -40,14 +40,19 @@ def run_half(plan, Ab, Bb, K, nnz, dtype):
 
 
 @pytest.mark.parametrize("dtype", [F16, BF16])
-@pytest.mark.parametrize("K", [32, 96, 256, 512])
-@pytest.mark.parametrize("case", ["blocky", "zipf"])
-def test_half_inputs_checkdata(dtype, K, case):
+@pytest.mark.parametrize("K", [32, 96, 128, 256, 512])
+@pytest.mark.parametrize("case", ["blocky", "zipf", "banded"])
+@pytest.mark.parametrize("layout", ["auto", "colmajor"])
+def test_half_inputs_checkdata(dtype, K, case, layout):
+    """fp16/bf16 A/B: row-block kernel for K = 128/256 (rows of 256/512 bytes), column-major
+    otherwise or when forced."""
     if case == "blocky":
         M, N, rp, ci = synth.block_mask(512, 16, 0.1, seed=7)
-    else:
+    elif case == "zipf":
         M, N, rp, ci = synth.random_rows(400, 3000, 50, seed=8, zipf=1.1)
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    else:  # cop20k-like banded FEM: many small row blocks, several piece phases per item
+        M, N, rp, ci = synth.banded_fem_like(6000, 22, seed=3, band=48)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout=layout)
     A = make_data(M * K)
     B = make_data(N * K)
     conv = to_bf16_bits if dtype == BF16 else to_f16_bits
