@@ -215,6 +215,7 @@ def main():
     prof = {} if args.no_split else plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
                                                   iters=20, stream=sp, dtype=dtype)
     P_gpu = dP.cpu().numpy()
+    st_after = plan.stats()  # the launch layout is built on the first SDDMM call
 
     s = 4 if dtype == F32 else 2
     flops_rank = 2.0 * nnz * K
@@ -233,7 +234,7 @@ def main():
         return
     # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
     rby = K * (4 if dtype == F32 else 2)
-    if rby in (256, 512):
+    if rby in (256, 512, 1024):
         kern = (f"k_sddmm_rb<{dtype},{rby},1024> (row-block LDS layout, {rby}-byte rows: "
                 "dense-tile MFMA + residual)")
     elif dtype == F32:
@@ -262,6 +263,7 @@ def main():
             "residual_nnz": st["num_residual"],
             "plan_build_s": round(plan_s, 3), "row_reorder_ms": round(st["row_reorder_ms"], 3),
             "col_reorder_ms": round(st["col_reorder_ms"], 3), "b_broadcast_ms": round(bcast_ms, 3),
+            "rowblock_layout": {k: st_after[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
         },
         "roofline": {
             "bound": "hbm",

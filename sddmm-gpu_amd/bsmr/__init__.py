@@ -56,10 +56,16 @@ class PlanStats(C.Structure):
                 ("num_sparse_thread_blocks", C.c_uint32),
                 ("exact_similarity_evals", C.c_uint64), ("total_similarity_evals", C.c_uint64),
                 ("row_reorder_ms", C.c_float), ("col_reorder_ms", C.c_float),
-                ("dense_items", C.c_uint32), ("residual_items", C.c_uint32)]
+                ("dense_items", C.c_uint32), ("residual_items", C.c_uint32),
+                ("rb_rows", C.c_uint32 * 3), ("rb_items", C.c_uint32 * 3),
+                ("rb_pieces", C.c_uint32 * 3)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = list(v) if hasattr(v, "__len__") else v
+        return d
 
 
 class EvalStats(C.Structure):

@@ -470,40 +470,74 @@ __device__ __forceinline__ f32x4 chunk_mfma(const f32x4 a, const f32x4 b, f32x4 
     }
 }
 
+// lanes per residual entry for a row size: 4 up to 512-byte rows, 8 for 1 KiB rows; every lane
+// then owns NC = RBY / (16 * G) <= 8 chunks of the row
+template <int RBY>
+struct RowGeom {
+    static constexpr u32 G = RBY >= 1024 ? 8 : 4;
+    static constexpr u32 NC = RBY / (16 * G);
+    static constexpr u32 NB = 16 / G;  // metadata batches per piece (RB_PIECE_MAX = 16 entries)
+};
+
+// value of lane I of the G-lane group in every lane of the group
+template <int G, int I>
+__device__ __forceinline__ u32 group_bcast(u32 v) {
+    if constexpr (G == 4)
+        return quad_bcast<I>(v);
+    else  // ds_swizzle bit mode: and 0x18 (the group), or I
+        return static_cast<u32>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x18 | (I << 5)));
+}
+
 // dense tile on the LDS image: load() gathers the tile's metadata and B operand (no LDS, so a
 // wave can issue it before the staging barrier), run() reads the A rows from LDS, runs the MFMAs
 // and scatters the 256 outputs. Lane group g takes chunk 16w + 4g + j at k-step 4w + j (any
-// k-permutation shared by A and B is valid), so the XOR of the LDS image spreads it.
+// k-permutation shared by A and B is valid), so the XOR of the LDS image spreads it. Rows of
+// 1 KiB (16 chunks per lane) are processed in two halves of 8 chunks.
 template <int DT, int RBY>
 struct DenseTileLds {
-    static constexpr int NK = RBY / 64;  // 16-byte chunks per lane
-    u32 lr, idx[4];
+    static constexpr int NK = RBY / 64;          // 16-byte chunks per lane
+    static constexpr int CH = NK > 8 ? 8 : NK;   // chunks held in registers at once
+    u32 lr, c, idx[4];
     __device__ __forceinline__ static u32 chunk(int kk, u32 g) {
         return 16 * (kk >> 2) + 4 * g + (kk & 3);
     }
-    __device__ __forceinline__ void load(const RbArgs& a, const u32 tile, const u32 q0,
-                                         f32x4 (&bv)[NK]) {
+    __device__ __forceinline__ void meta(const RbArgs& a, const u32 tile, const u32 q0) {
         const u32 l = __lane_id(), rr = l & 15, g = l >> 4;
         const u32 p = a.tilePanel[tile].x;
-        const u32 c = a.denseCols[tile * 16 + rr];
+        c = a.denseCols[tile * 16 + rr];
         const u32* bvals = a.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
 #pragma unroll
         for (int r = 0; r < 4; ++r) idx[r] = bvals[16 * r];
         lr = p * 16 - q0 + rr;
+    }
+    // B chunks [k0, k0 + CH)
+    __device__ __forceinline__ void loadB(const RbArgs& a, const int k0, f32x4 (&bv)[CH]) const {
+        const u32 g = __lane_id() >> 4;
         const bool cvalid = c < a.N;
         const char* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * RBY;
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) bv[kk] = cvalid ? ld16(bcol + 16 * chunk(kk, g)) : f32x4{0, 0, 0, 0};
+        for (int kk = 0; kk < CH; ++kk)
+            bv[kk] = cvalid ? ld16(bcol + 16 * chunk(k0 + kk, g)) : f32x4{0, 0, 0, 0};
     }
-    __device__ __forceinline__ void run(const RbArgs& a, const char* As, const f32x4 (&bv)[NK]) const {
+    __device__ __forceinline__ void load(const RbArgs& a, const u32 tile, const u32 q0,
+                                         f32x4 (&bv)[CH]) {
+        meta(a, tile, q0);
+        loadB(a, 0, bv);
+    }
+    // bv: the first CH chunks (from load); later halves are loaded here
+    __device__ __forceinline__ void run(const RbArgs& a, const char* As, f32x4 (&bv)[CH]) const {
         const u32 g = __lane_id() >> 4;
         const char* arow = As + lr * RBY;
         f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) {
-            const f32x4 av = ld16(arow + 16 * lds_chunk(lr, chunk(kk, g)));
-            f32x4& acc = (kk & 1) ? acc1 : acc0;
-            acc = chunk_mfma<DT>(av, bv[kk], acc);
+        for (int k0 = 0; k0 < NK; k0 += CH) {
+            if (k0) loadB(a, k0, bv);
+#pragma unroll
+            for (int kk = 0; kk < CH; ++kk) {
+                const f32x4 av = ld16(arow + 16 * lds_chunk(lr, chunk(k0 + kk, g)));
+                f32x4& acc = (kk & 1) ? acc1 : acc0;
+                acc = chunk_mfma<DT>(av, bv[kk], acc);
+            }
         }
         const f32x4 acc = acc0 + acc1;
 #pragma unroll
@@ -512,72 +546,82 @@ struct DenseTileLds {
     }
 };
 
-// B pieces of the group's column (lane s: chunks 4 * ((f + j) mod NC) + s, f < NC)
+// B pieces of the group's column (lane s: chunks G * ((f + j) mod NC) + s, f < NC)
 template <int RBY>
 __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const u32 sub,
-                                          const u32 (&rot)[RBY / 64], f32x4 (&bv)[RBY / 64]) {
+                                          const u32 (&rot)[RowGeom<RBY>::NC],
+                                          f32x4 (&bv)[RowGeom<RBY>::NC]) {
     const u32 bb = col * RBY + 16 * sub;
 #pragma unroll
-    for (u32 f = 0; f < RBY / 64; ++f) bv[f] = ld16(a.B + (bb + rot[f]));
+    for (u32 f = 0; f < RowGeom<RBY>::NC; ++f) bv[f] = ld16(a.B + (bb + rot[f]));
 }
 
 // a column-run piece of a row-group: entries [first, first + len), len <= RB_PIECE_MAX = 16, all
-// in one column. Lane s of the group holds the metadata of entries first + 4k + s (k < 4).
+// in one column. Lane s of the group holds the metadata of entries first + G*k + s.
+template <int RBY>
 struct Piece {
     u32 first, len;
-    u32 mm[4], mo[4];
+    u32 mm[RowGeom<RBY>::NB], mo[RowGeom<RBY>::NB];
 };
 
 template <int RBY>
 __device__ __forceinline__ void load_piece(const RbArgs& a, const u32 pi, const u32 sub,
-                                           const u32 (&rot)[RBY / 64], f32x4 (&bv)[RBY / 64],
-                                           Piece& pc) {
+                                           const u32 (&rot)[RowGeom<RBY>::NC],
+                                           f32x4 (&bv)[RowGeom<RBY>::NC], Piece<RBY>& pc) {
+    constexpr u32 G = RowGeom<RBY>::G;
     const uint2 d = a.pieces[pi];
     pc.first = d.x;
     pc.len = (d.y >> 22) + 1;
     load_bcol<RBY>(a, d.y & 0x3FFFFFu, sub, rot, bv);
 #pragma unroll
-    for (u32 k = 0; k < 4; ++k) {
-        const u32 e = 4 * k + sub;
+    for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
+        const u32 e = G * k + sub;
         pc.mm[k] = e < pc.len ? a.meta[pc.first + e] : 0u;
         pc.mo[k] = e < pc.len ? a.out[pc.first + e] : 0u;
     }
 }
 
-// Step i of a batch of 4 computes entry 4k + i in all 4 lanes; lane i keeps it, so a batch ends
-// in one store instruction for 4 entries per group (64 outputs per full wave).
+// Step i of a batch of G computes entry G*k + i in all G lanes; lane i keeps it, so a batch ends
+// in one store instruction for G entries per group (64 outputs per full wave).
 template <int DT, int RBY>
-__device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As, const Piece& pc,
-                                               const u32 sub, const u32 (&rot)[RBY / 64],
-                                               const f32x4 (&bv)[RBY / 64]) {
-    constexpr u32 NC = RBY / 64;
+__device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
+                                               const Piece<RBY>& pc, const u32 sub,
+                                               const u32 (&rot)[RowGeom<RBY>::NC],
+                                               const f32x4 (&bv)[RowGeom<RBY>::NC]) {
+    constexpr u32 G = RowGeom<RBY>::G, NC = RowGeom<RBY>::NC;
 #pragma unroll
-    for (u32 k = 0; k < 4; ++k) {
-        if (4 * k >= pc.len) break;
-        const u32 nb = min(4u, pc.len - 4 * k);
+    for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
+        if (G * k >= pc.len) break;
+        const u32 nb = min(G, pc.len - G * k);
         float res = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < static_cast<int>(G); ++i) {
             if (static_cast<u32>(i) >= nb) break;
             u32 m;
             switch (i) {
-                case 0: m = quad_bcast<0>(pc.mm[k]); break;
-                case 1: m = quad_bcast<1>(pc.mm[k]); break;
-                case 2: m = quad_bcast<2>(pc.mm[k]); break;
-                default: m = quad_bcast<3>(pc.mm[k]); break;
+#define BSMR_C(I) \
+    case I: m = group_bcast<G, (I < G ? I : 0)>(pc.mm[k]); break;
+                BSMR_C(0) BSMR_C(1) BSMR_C(2) BSMR_C(3) BSMR_C(4) BSMR_C(5) BSMR_C(6)
+#undef BSMR_C
+                default: m = group_bcast<G, G - 1>(pc.mm[k]); break;
             }
             const u32 lr = m >> 22;
             const u32 ab = lr * RBY + 16 * (sub ^ (lr & 3));
-            f32x4 av[NC];  // all NC reads in flight before the first FMA
-#pragma unroll
-            for (u32 f = 0; f < NC; ++f) av[f] = ld16(As + (ab + rot[f]));
             f32x2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+            constexpr u32 H = NC > 4 ? NC / 2 : NC;  // LDS reads in flight per half
 #pragma unroll
-            for (u32 f = 0; f < NC; ++f) chunk_dot<DT>(av[f], bv[f], acc0, acc1);
+            for (u32 h = 0; h < NC; h += H) {
+                f32x4 av[H];
+#pragma unroll
+                for (u32 f = 0; f < H; ++f) av[f] = ld16(As + (ab + rot[h + f]));
+#pragma unroll
+                for (u32 f = 0; f < H; ++f) chunk_dot<DT>(av[f], bv[h + f], acc0, acc1);
+            }
             const f32x2 acc = acc0 + acc1;
             float sm = acc.x + acc.y;
-            sm += dppf<0xB1>(sm);  // quad_perm [1,0,3,2]
-            sm += dppf<0x4E>(sm);  // quad_perm [2,3,0,1]
+            sm += dppf<0xB1>(sm);                         // quad_perm [1,0,3,2]
+            sm += dppf<0x4E>(sm);                         // quad_perm [2,3,0,1]
+            if constexpr (G == 8) sm += dppf<0x141>(sm);  // row_half_mirror: the other quad
             if (sub == static_cast<u32>(i)) res = sm;
         }
         if (sub < nb) a.P[pc.mo[k]] = res;
@@ -593,30 +637,32 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         a.B += blockIdx.y * a.bB;
         a.P += blockIdx.y * a.bP;
     }
-    constexpr u32 NC = RBY / 64;  // chunks per lane (tile or row-group)
-    constexpr u32 NW = NT / 64;   // waves per workgroup
-    constexpr u32 NG = NT / 4;    // residual row-groups
+    using Geo = RowGeom<RBY>;
+    constexpr u32 G = Geo::G, NC = Geo::NC;  // lanes per entry, chunks per lane
+    constexpr u32 NW = NT / 64;               // waves per workgroup
+    constexpr u32 NG = NT / G;                // residual row-groups
+    constexpr u32 TC = DenseTileLds<DT, RBY>::CH;
     const unsigned long long t0 = rtime(a.trace);
     const uint4 it = a.items[blockIdx.x];
     const u32 pend = a.itemEnd[blockIdx.x];
     if (it.y == it.z && it.w == pend) return;  // padding item (uniform across the workgroup)
     const u32 q0 = it.x * a.RB;
-    const u32 tid = threadIdx.x, w = tid >> 6, sub = tid & 3, j = (tid >> 2) & 15;
-    // every wave takes (at most) one dense tile and its 16 row-groups one residual piece each per
+    const u32 tid = threadIdx.x, w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
+    // every wave takes (at most) one dense tile and its row-groups one residual piece each per
     // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
     // staging loads so all of it is in flight together
     const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
     const u32 np = (a.mode & 2) ? pend - it.w : 0u;
-    const u32 gr = tid >> 2;
-    u32 rot[NC];  // residual: byte offset of the 64-byte quad the lane visits at step f
+    const u32 gr = tid / G;
+    u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
 #pragma unroll
-    for (u32 f = 0; f < NC; ++f) rot[f] = 64u * ((f + j) % NC);
-    f32x4 tb[NC], pre[NC];
+    for (u32 f = 0; f < NC; ++f) rot[f] = 16u * G * ((f + j) % NC);
+    f32x4 tb[TC], pre[NC];
     DenseTileLds<DT, RBY> dt;
     // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
     const u32 tw = NW - 1 - w;
     if (tw < ntile) dt.load(a, it.y + tw, q0, tb);
-    Piece pc;
+    Piece<RBY> pc;
     pc.len = 0;
     if (gr < np) load_piece<RBY>(a, it.w + gr, sub, rot, pre, pc);
     // stage the row block by LDS-DMA: each wave-instruction fills one contiguous KiB of the image
@@ -652,15 +698,24 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     }
     if (tw < ntile) dt.run(a, As, tb);
     const unsigned long long td = rtime(a.trace);
-    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
-    // later phases (items with more pieces than row-groups): the extra pieces are the shortest
-    // and go to the groups that had the shortest phase-0 pieces
-    for (u32 ph = 1; ph * NG < np; ++ph) {
+    // later phases (items with more pieces than row-groups, e.g. short column runs): the extra
+    // pieces are the shortest and go to the groups that had the shortest phase-0 pieces; phase
+    // ph's piece and B column are loaded while phase ph - 1 computes (two register sets)
+    Piece<RBY> pn;
+    f32x4 nb[NC];
+    auto fetch = [&](const u32 ph) {
         const u32 pi = ph * NG + (NG - 1 - gr);
-        if (pi < np) {
-            load_piece<RBY>(a, it.w + pi, sub, rot, pre, pc);
-            residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
-        }
+        pn.len = 0;
+        if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
+    };
+    if (NG < np) fetch(1);
+    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+    for (u32 ph = 1; ph * NG < np; ++ph) {
+        pc = pn;
+#pragma unroll
+        for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
+        if ((ph + 1) * NG < np) fetch(ph + 1);
+        if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     }
     for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
         dt.load(a, t, q0, tb);
@@ -734,16 +789,17 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
     return a;
 }
 
-// (K, dtype) -> row-block layout slot by row bytes (0: 256 B, 1: 512 B); -1: column-major path
+// (K, dtype) -> row-block layout slot by row bytes (0: 256 B, 1: 512 B, 2: 1 KiB); -1: the
+// column-major path
 int rb_slot(const Plan& p, u32 K, int dtype) {
     if (p.N > (1u << 22) || !p.use_rowblock) return -1;
-    if (dtype == BSMR_F32) return K == 64 ? 0 : K == 128 ? 1 : -1;
-    return K == 128 ? 0 : K == 256 ? 1 : -1;
+    const u32 rby = K * (dtype == BSMR_F32 ? 4u : 2u);
+    return rby == 256 ? 0 : rby == 512 ? 1 : rby == 1024 ? 2 : -1;
 }
 
 int ensure_rb_layout(const Plan& p, int slot) {
     std::lock_guard<std::mutex> g(p.layout_mu);
-    const u32 rby = slot == 0 ? 256 : 512;
+    const u32 rby = 256u << slot;
     if (p.rbl[slot].rowBytes == rby) return BSMR_OK;
     return p.build_rowblock_layout(slot, rby);
 }
@@ -780,7 +836,8 @@ int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
 #define BSMR_RB(DT, RBY) (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>)
-#define BSMR_RB2(DT) (L.rowBytes == 256 ? BSMR_RB(DT, 256) : BSMR_RB(DT, 512))
+#define BSMR_RB2(DT) \
+    (L.rowBytes == 256 ? BSMR_RB(DT, 256) : L.rowBytes == 512 ? BSMR_RB(DT, 512) : BSMR_RB(DT, 1024))
     switch (dtype) {
         case BSMR_F32: fn = BSMR_RB2(0); break;
         case BSMR_F16: fn = BSMR_RB2(1); break;

@@ -22,24 +22,31 @@ def main():
     ap.add_argument("--workload", default="nips_like")
     ap.add_argument("--layout", default="auto", choices=["auto", "rowblock", "colmajor"])
     ap.add_argument("--lds-kb", type=int, default=0)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     args = ap.parse_args()
     import torch
 
+    import bsmr
     from bsmr import Plan, make_data, synth
 
     M, N, rp, ci = getattr(synth, args.workload)()
     K = args.K
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout,
                 lds_budget_kb=args.lds_kb)
-    dA = torch.from_numpy(make_data(M * K)).cuda()
-    dB = torch.from_numpy(make_data(N * K)).cuda()
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
+    code = {"f32": bsmr.F32, "f16": bsmr.F16, "bf16": bsmr.BF16}[args.dtype]
+    dA = torch.from_numpy(make_data(M * K)).cuda().to(tdt)
+    dB = torch.from_numpy(make_data(N * K)).cuda().to(tdt)
     dP = torch.zeros(len(ci), dtype=torch.float32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s)
-    r = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=args.iters, stream=s)
+    plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s, dtype=code)
+    r = plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), iters=args.iters, stream=s,
+                     dtype=code)
     torch.cuda.synchronize()
     st = plan.stats()
-    print(json.dumps({"M": M, "N": N, "nnz": len(ci), "K": K, "layout": args.layout,
+    print(json.dumps({"M": M, "N": N, "nnz": len(ci), "K": K, "dtype": args.dtype,
+                      "workload": args.workload, "layout": args.layout,
+                      "rb": {k: st[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
                       "lds_kb": args.lds_kb, "timing_ms": r,
                       "dense_items": st["dense_items"], "residual_slots_hint": st["residual_items"],
                       "dense_tiles": st["num_dense_tiles"], "residual": st["num_residual"]}))

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--layout", default="auto")
     ap.add_argument("--lds-kb", type=int, default=0)
     ap.add_argument("--dump", default="")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     args = ap.parse_args()
     os.environ["BSMR_DIAG"] = str(int(os.environ.get("BSMR_DIAG", "0")) | 32)
     import torch
@@ -37,12 +38,14 @@ def main():
     M, N, rp, ci = getattr(synth, args.workload)()
     K = args.K
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout, lds_budget_kb=args.lds_kb)
-    dA = torch.from_numpy(make_data(M * K)).cuda()
-    dB = torch.from_numpy(make_data(N * K)).cuda()
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
+    code = {"f32": bsmr.F32, "f16": bsmr.F16, "bf16": bsmr.BF16}[args.dtype]
+    dA = torch.from_numpy(make_data(M * K)).cuda().to(tdt)
+    dB = torch.from_numpy(make_data(N * K)).cuda().to(tdt)
     dP = torch.zeros(len(ci), dtype=torch.float32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(10):
-        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s)
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s, dtype=code)
     torch.cuda.synchronize()
     L = bsmr.lib()
     L.bsmr_debug_trace.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
@@ -59,7 +62,9 @@ def main():
     base = t0.min()
     us = 0.01  # 100 MHz ticks -> us
     xcc = (t[:, 3] >> np.uint64(60)).astype(np.int64) & 0xF
-    out = {"K": K, "layout": args.layout, "lds_kb": args.lds_kb, "waves": int(len(t)),
+    out = {"K": K, "workload": args.workload, "dtype": args.dtype, "layout": args.layout,
+           "lds_kb": args.lds_kb, "waves": int(len(t)),
+           "rb": {k: plan.stats()[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
            "span_us": round(float((t1.max() - base) * us), 3),
            "start_us": pct((t0 - base) * us), "life_us": pct((t1 - t0) * us),
            "mid_us": pct((tm - t0) * us), "dense_us": pct((td - tm) * us),
