@@ -234,7 +234,7 @@ def main():
         return
     # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
     rby = K * (4 if dtype == F32 else 2)
-    if rby in (256, 512, 1024):
+    if rby in (256, 512, 1024, 2048):
         kern = (f"k_sddmm_rb<{dtype},{rby},1024> (row-block LDS layout, {rby}-byte rows: "
                 "dense-tile MFMA + residual)")
     elif dtype == F32:

@@ -119,9 +119,9 @@ typedef struct {
     float row_reorder_ms;            /* bsmr_rowReordering */
     float col_reorder_ms;            /* bsmr_colReordering (incl. tile layout) */
     uint32_t dense_items, residual_items;  /* work-list sizes of the SDDMM launch */
-    /* row-block layouts built so far (index 0/1/2: rows of 256/512/1024 bytes; 0 = not built):
-     * rows per block, workgroup items (incl. per-XCD padding), column-run pieces */
-    uint32_t rb_rows[3], rb_items[3], rb_pieces[3];
+    /* row-block layouts built so far (index 0..3: rows of 256/512/1024/2048 bytes; 0 = not
+     * built): rows per block, workgroup items (incl. per-XCD padding), column-run pieces */
+    uint32_t rb_rows[4], rb_items[4], rb_pieces[4];
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

@@ -57,8 +57,8 @@ class PlanStats(C.Structure):
                 ("exact_similarity_evals", C.c_uint64), ("total_similarity_evals", C.c_uint64),
                 ("row_reorder_ms", C.c_float), ("col_reorder_ms", C.c_float),
                 ("dense_items", C.c_uint32), ("residual_items", C.c_uint32),
-                ("rb_rows", C.c_uint32 * 3), ("rb_items", C.c_uint32 * 3),
-                ("rb_pieces", C.c_uint32 * 3)]
+                ("rb_rows", C.c_uint32 * 4), ("rb_items", C.c_uint32 * 4),
+                ("rb_pieces", C.c_uint32 * 4)]
 
     def as_dict(self):
         d = {}

@@ -122,7 +122,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
     s->col_reorder_ms = p.col_ms;
     s->dense_items = p.nDenseItems;
     s->residual_items = p.nResItems;
-    for (int i = 0; i < Plan::N_RB_LAYOUTS && i < 3; ++i) {
+    for (int i = 0; i < Plan::N_RB_LAYOUTS && i < 4; ++i) {
         const Plan::RowBlockLayout& L = p.rbl[i];
         s->rb_rows[i] = L.rowBytes ? L.RB : 0;
         s->rb_items[i] = L.rowBytes ? L.nItems : 0;

@@ -86,7 +86,7 @@ struct Plan {
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}
     };
-    static constexpr int N_RB_LAYOUTS = 3;  // rows of 256, 512 and 1024 bytes
+    static constexpr int N_RB_LAYOUTS = 4;  // rows of 256, 512, 1024 and 2048 bytes
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
     int build_rowblock_layout(int slot, u32 rowBytes) const;
 

@@ -470,11 +470,11 @@ __device__ __forceinline__ f32x4 chunk_mfma(const f32x4 a, const f32x4 b, f32x4 
     }
 }
 
-// lanes per residual entry for a row size: 4 up to 512-byte rows, 8 for 1 KiB rows; every lane
-// then owns NC = RBY / (16 * G) <= 8 chunks of the row
+// lanes per residual entry for a row size: 4 up to 512-byte rows, 8 for 1 KiB, 16 for 2 KiB rows;
+// every lane then owns NC = RBY / (16 * G) <= 8 chunks of the row
 template <int RBY>
 struct RowGeom {
-    static constexpr u32 G = RBY >= 1024 ? 8 : 4;
+    static constexpr u32 G = RBY >= 2048 ? 16 : RBY >= 1024 ? 8 : 4;
     static constexpr u32 NC = RBY / (16 * G);
     static constexpr u32 NB = 16 / G;  // metadata batches per piece (RB_PIECE_MAX = 16 entries)
 };
@@ -484,8 +484,10 @@ template <int G, int I>
 __device__ __forceinline__ u32 group_bcast(u32 v) {
     if constexpr (G == 4)
         return quad_bcast<I>(v);
-    else  // ds_swizzle bit mode: and 0x18 (the group), or I
+    else if constexpr (G == 8)  // ds_swizzle bit mode: and 0x18 (the group), or I
         return static_cast<u32>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x18 | (I << 5)));
+    else  // a whole DPP row
+        return row_bcast<I>(v);
 }
 
 // dense tile on the LDS image: load() gathers the tile's metadata and B operand (no LDS, so a
@@ -601,7 +603,8 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             switch (i) {
 #define BSMR_C(I) \
     case I: m = group_bcast<G, (I < G ? I : 0)>(pc.mm[k]); break;
-                BSMR_C(0) BSMR_C(1) BSMR_C(2) BSMR_C(3) BSMR_C(4) BSMR_C(5) BSMR_C(6)
+                BSMR_C(0) BSMR_C(1) BSMR_C(2) BSMR_C(3) BSMR_C(4) BSMR_C(5) BSMR_C(6) BSMR_C(7)
+                BSMR_C(8) BSMR_C(9) BSMR_C(10) BSMR_C(11) BSMR_C(12) BSMR_C(13) BSMR_C(14)
 #undef BSMR_C
                 default: m = group_bcast<G, G - 1>(pc.mm[k]); break;
             }
@@ -621,7 +624,8 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             float sm = acc.x + acc.y;
             sm += dppf<0xB1>(sm);                         // quad_perm [1,0,3,2]
             sm += dppf<0x4E>(sm);                         // quad_perm [2,3,0,1]
-            if constexpr (G == 8) sm += dppf<0x141>(sm);  // row_half_mirror: the other quad
+            if constexpr (G >= 8) sm += dppf<0x141>(sm);   // row_half_mirror: the other quad
+            if constexpr (G == 16) sm += dppf<0x140>(sm);  // row_mirror: the other half-row
             if (sub == static_cast<u32>(i)) res = sm;
         }
         if (sub < nb) a.P[pc.mo[k]] = res;
@@ -666,24 +670,30 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     pc.len = 0;
     if (gr < np) load_piece<RBY>(a, it.w + gr, sub, rot, pre, pc);
     // stage the row block by LDS-DMA: each wave-instruction fills one contiguous KiB of the image
-    // (RPB rows); lane l supplies row lr = RPB * b + l / LPR at physical chunk pc = l % LPR, read
-    // from the logical chunk lds_chunk(lr, pc) of A[rows[q0 + lr]] (the XOR is an involution)
+    // (64 chunks of the row-major image); lane l supplies image chunk x = 64 b + l, i.e. row
+    // lr = x / NCH at physical chunk pc = x % NCH, read from the logical chunk lds_chunk(lr, pc)
+    // of A[rows[q0 + lr]] (the XOR is an involution). The row indices of the wave's blocks are
+    // loaded once, one per lane, and handed to the block's lanes with ds_bpermute.
     {
-        constexpr u32 LPR = RBY / 16, RPB = 64 / LPR;
+        constexpr u32 NCH = RBY / 16;
+        constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
         // KiB blocks per wave (max): NT = 512 is launched only for images <= 80 KiB
         constexpr u32 MAXB = ((NT == 1024 ? 160u : 80u) + NW - 1) / NW;
-        const u32 lane = tid & 63, nblk = a.RB / RPB;
-        u32 src[MAXB];
-#pragma unroll
-        for (u32 i = 0; i < MAXB; ++i) {
-            const u32 b = w + i * NW, lr = b * RPB + lane / LPR, q = q0 + lr;
-            src[i] = (b < nblk && q < a.R) ? a.rows[q] : 0u;
+        static_assert(MAXB * NR <= 64, "one row index per lane");
+        const u32 lane = tid & 63, nblk = a.RB * NCH / 64;
+        u32 rowv = 0;
+        {
+            const u32 i = lane / NR, b = w + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
+            if (i < MAXB && b < nblk && q < a.R) rowv = a.rows[q];
         }
 #pragma unroll
         for (u32 i = 0; i < MAXB; ++i) {
-            const u32 b = w + i * NW, lr = b * RPB + lane / LPR;
-            if (b < nblk) {
-                const char* g = a.A + static_cast<size_t>(src[i]) * RBY + 16 * lds_chunk(lr, lane % LPR);
+            const u32 b = w + i * NW;
+            if (b < nblk) {  // wave-uniform
+                const u32 x = 64 * b + lane, lr = x / NCH;
+                const u32 src = static_cast<u32>(__builtin_amdgcn_ds_bpermute(
+                    static_cast<int>(4 * (i * NR + (NCH >= 64 ? 0 : lane / NCH))), static_cast<int>(rowv)));
+                const char* g = a.A + static_cast<size_t>(src) * RBY + 16 * lds_chunk(lr, x % NCH);
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                                  (__attribute__((address_space(3))) void*)(As + 1024 * b),
                                                  16, 0, 0);
@@ -789,12 +799,12 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
     return a;
 }
 
-// (K, dtype) -> row-block layout slot by row bytes (0: 256 B, 1: 512 B, 2: 1 KiB); -1: the
-// column-major path
+// (K, dtype) -> row-block layout slot by row bytes (0..3: 256 B .. 2 KiB); -1: the column-major
+// path
 int rb_slot(const Plan& p, u32 K, int dtype) {
     if (p.N > (1u << 22) || !p.use_rowblock) return -1;
     const u32 rby = K * (dtype == BSMR_F32 ? 4u : 2u);
-    return rby == 256 ? 0 : rby == 512 ? 1 : rby == 1024 ? 2 : -1;
+    return rby == 256 ? 0 : rby == 512 ? 1 : rby == 1024 ? 2 : rby == 2048 ? 3 : -1;
 }
 
 int ensure_rb_layout(const Plan& p, int slot) {
@@ -836,8 +846,11 @@ int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
 #define BSMR_RB(DT, RBY) (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>)
-#define BSMR_RB2(DT) \
-    (L.rowBytes == 256 ? BSMR_RB(DT, 256) : L.rowBytes == 512 ? BSMR_RB(DT, 512) : BSMR_RB(DT, 1024))
+#define BSMR_RB2(DT)                                                                   \
+    (L.rowBytes == 256    ? BSMR_RB(DT, 256)                                              \
+     : L.rowBytes == 512  ? BSMR_RB(DT, 512)                                              \
+     : L.rowBytes == 1024 ? BSMR_RB(DT, 1024)                                             \
+                          : BSMR_RB(DT, 2048))
     switch (dtype) {
         case BSMR_F32: fn = BSMR_RB2(0); break;
         case BSMR_F16: fn = BSMR_RB2(1); break;

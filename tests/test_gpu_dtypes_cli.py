@@ -152,3 +152,18 @@ def test_cli_test_mode_writes_reference_log_files(tmp_path):
     text = open(os.path.join(tmp_path, "BSMR_k_128_a_0.3_d_0.3.log")).read()
     assert text.startswith("\n---New data---\n")
     assert _log_fields(text)["bsmr_delta"] == "0.30"
+
+
+@pytest.mark.parametrize("dtype", [F16, BF16])
+def test_half_k1024_rowblock(dtype):
+    """2 KiB rows (K = 1024 half): the 16-lanes-per-entry row-block kernel."""
+    M, N, rp, ci = synth.random_rows(700, 2500, 60, seed=21, zipf=1.1)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    K = 1024
+    conv = to_bf16_bits if dtype == BF16 else to_f16_bits
+    Ab, Ar = conv(make_data(M * K))
+    Bb, Br = conv(make_data(N * K))
+    P = run_half(plan, Ab, Bb, K, len(ci), dtype)
+    assert plan.stats()["rb_items"][3] > 0
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, Ar, Br)
+    assert O.check_data(ref, P) == 0
