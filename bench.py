@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--delta", type=float, default=0.3)
     ap.add_argument("--scale", type=float, default=1.0, help="C4 size factor")
     ap.add_argument("--mask", default="uniform", choices=["uniform", "block"], help="C5 mask")
+    ap.add_argument("--layout", default="auto", choices=["auto", "rowblock", "colmajor"],
+                    help="SDDMM launch layout (bsmr_plan_options.layout)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-split", action="store_true",
                     help="skip the cold steps and the dense/residual split launches (rocprof runs: "
@@ -145,7 +147,8 @@ def main():
     (M, N, rp, ci), K, dtype, desc = workload(args)
     nnz = len(ci)
     t0 = time.perf_counter()
-    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, device=dev.index)
+    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, device=dev.index,
+                layout=args.layout)
     plan_s = time.perf_counter() - t0
     st = plan.stats()
 
@@ -234,7 +237,8 @@ def main():
         return
     # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
     rby = K * (4 if dtype == F32 else 2)
-    if rby in (256, 512, 1024, 2048):
+    tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
+    if rby in (256, 512, 1024, 2048) and args.layout != "colmajor" and not tile_dominated:
         kern = (f"k_sddmm_rb<{dtype},{rby},1024> (row-block LDS layout, {rby}-byte rows: "
                 "dense-tile MFMA + residual)")
     elif dtype == F32:

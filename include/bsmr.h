@@ -84,8 +84,10 @@ typedef struct {
     uint32_t lds_budget_kb;   /* LDS per row-block workgroup, 16..160 KiB; 0 = default (144) */
 } bsmr_plan_options;
 
-/* AUTO = ROWBLOCK: A rows staged in LDS per row block, K in {64, 128, 256, 512}, column-major
- * residual slots for other K. COLMAJOR: column-major slots for every K. Results are identical
+/* AUTO: A rows staged in LDS per row block for rows of 256 B .. 2 KiB (fp32 K = 64..512,
+ * fp16/bf16 K = 128..1024), unless dense tiles carry over 3/4 of the work (then one tile per
+ * wave, column-major residual slots); the column-major path for other K. ROWBLOCK: row blocks
+ * whenever the row size allows. COLMAJOR: column-major slots for every K. Results are identical
  * up to fp32 summation order (checkData tolerance). */
 enum { BSMR_LAYOUT_AUTO = 0, BSMR_LAYOUT_ROWBLOCK = 1, BSMR_LAYOUT_COLMAJOR = 2 };
 

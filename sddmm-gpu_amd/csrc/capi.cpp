@@ -63,6 +63,7 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
         return fail(BSMR_ERR_INVALID);
     }
     p.use_rowblock = o.layout != BSMR_LAYOUT_COLMAJOR;
+    p.force_rowblock = o.layout == BSMR_LAYOUT_ROWBLOCK;
     if (o.lds_budget_kb) p.rb_lds_kb = o.lds_budget_kb;
     if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
     u64 free_mem = o.free_mem_bytes;

@@ -921,7 +921,7 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
             cost[i] = (se1[i] - se0[i]) + 16.0 * (st1[i] - st0[i]);
         }
     }
-    // chunks: one round of workgroup slots (Q items) unless items would drop below ~512 units. A
+    // chunks: one round of workgroup slots (Q items) unless items would drop below ~128 units. A
     // row block big enough for >= 8 items is split by the XCD column ranges (its items then read B
     // from their own XCD's L2); a smaller one (e.g. banded matrices: many row blocks of few
     // entries) is cut along its whole column-sorted entry list, and its items balance the XCD list
@@ -931,7 +931,8 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
     std::vector<std::vector<u32>> lends(XCD_BUCKETS);
     double total = 0;
     for (double c : cost) total += c;
-    const u32 Q = std::max<u32>(1, std::min<u32>(perBucket * XCD_BUCKETS, static_cast<u32>(total / 512.0)));
+    // an item is worth its row-block staging from ~128 cost units (entries; a tile counts 16)
+    const u32 Q = std::max<u32>(1, std::min<u32>(perBucket * XCD_BUCKETS, static_cast<u32>(total / 128.0)));
     const double target = total / Q;
     std::vector<double> cb(nRB, 0.0);
     std::vector<char> split(nRB, 0);

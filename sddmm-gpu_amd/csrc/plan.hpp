@@ -34,6 +34,7 @@ struct Plan {
     // launch layout (bsmr_plan_options.layout): row-block LDS items for K in {64, 128, 256, 512}
     // unless BSMR_LAYOUT_COLMAJOR; the column-major residual slots for every other K
     bool use_rowblock = true;
+    bool force_rowblock = false;  // BSMR_LAYOUT_ROWBLOCK: also for tile-dominated plans
     u32 rb_lds_kb = 144;  // LDS budget of a row-block workgroup (bsmr_plan_options.lds_budget_kb)
     u32 diag = 0;  // BSMR_DIAG profiling ablations (wrong results; never set in normal use)
     u32 cluster_batch = 512;

@@ -803,6 +803,11 @@ SddmmArgs make_args(const Plan& p, const void* dA, const void* dB, u32 K, float*
 // path
 int rb_slot(const Plan& p, u32 K, int dtype) {
     if (p.N > (1u << 22) || !p.use_rowblock) return -1;
+    // tile-dominated plans (e.g. 16x16 block masks): one tile per wave with A from L2 beats
+    // staging row blocks (C5 block mask: 8.9 vs 11.1 us); row blocks pay off once the residual
+    // carries a quarter of the work (a tile ~ 16 entries)
+    if (!p.force_rowblock && static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16)
+        return -1;
     const u32 rby = K * (dtype == BSMR_F32 ? 4u : 2u);
     return rby == 256 ? 0 : rby == 512 ? 1 : rby == 1024 ? 2 : rby == 2048 ? 3 : -1;
 }

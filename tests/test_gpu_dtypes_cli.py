@@ -42,7 +42,7 @@ def run_half(plan, Ab, Bb, K, nnz, dtype):
 @pytest.mark.parametrize("dtype", [F16, BF16])
 @pytest.mark.parametrize("K", [32, 96, 128, 256, 512])
 @pytest.mark.parametrize("case", ["blocky", "zipf", "banded"])
-@pytest.mark.parametrize("layout", ["auto", "colmajor"])
+@pytest.mark.parametrize("layout", ["rowblock", "colmajor"])
 def test_half_inputs_checkdata(dtype, K, case, layout):
     """fp16/bf16 A/B: row-block kernel for K = 128/256 (rows of 256/512 bytes), column-major
     otherwise or when forced."""

@@ -148,8 +148,8 @@ def test_sddmm_nips_like_checkdata(K, layout, lds_kb):
     assert O.check_data(ref, P) == 0
 
 
-@pytest.mark.parametrize("K,layout", [(128, "auto"), (128, "colmajor"), (64, "auto"),
-                                      (256, "auto")])
+@pytest.mark.parametrize("K,layout", [(128, "auto"), (128, "colmajor"), (128, "rowblock"),
+                                      (64, "rowblock"), (256, "rowblock"), (512, "rowblock")])
 def test_sddmm_blocky_dense_tiles(K, layout):
     M, N, rp, ci = small_cases()["blocky"]
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout=layout)
