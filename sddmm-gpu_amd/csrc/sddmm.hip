@@ -476,7 +476,7 @@ template <int RBY>
 struct RowGeom {
     static constexpr u32 G = RBY >= 2048 ? 16 : RBY >= 1024 ? 8 : 4;
     static constexpr u32 NC = RBY / (16 * G);
-    static constexpr u32 NB = 16 / G;  // metadata batches per piece (RB_PIECE_MAX = 16 entries)
+    static constexpr u32 NB = (RB_PIECE_MAX + G - 1) / G;  // metadata batches per piece
 };
 
 // value of lane I of the G-lane group in every lane of the group
@@ -558,7 +558,7 @@ __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const 
     for (u32 f = 0; f < RowGeom<RBY>::NC; ++f) bv[f] = ld16(a.B + (bb + rot[f]));
 }
 
-// a column-run piece of a row-group: entries [first, first + len), len <= RB_PIECE_MAX = 16, all
+// a column-run piece of a row-group: entries [first, first + len), len <= RB_PIECE_MAX, all
 // in one column. Lane s of the group holds the metadata of entries first + G*k + s.
 template <int RBY>
 struct Piece {
