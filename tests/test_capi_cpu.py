@@ -25,6 +25,17 @@ def test_library_exports_every_header_symbol():
     assert L.bsmr_abi_version() == 1
 
 
+def test_rocsparse_baseline_exports_every_header_symbol():
+    from bsmr import vendor
+
+    header = open(os.path.join(ROOT, "include", "bsmr_rocsparse.h")).read()
+    declared = set(re.findall(r"\b(bsmr_rocsparse_[a-z_0-9]+)\s*\(", header))
+    L = vendor.lib()
+    missing = [s for s in sorted(declared) if not hasattr(L, s)]
+    assert not missing, missing
+    assert declared == set(vendor.EXPORTS), declared ^ set(vendor.EXPORTS)
+
+
 def test_plan_options_defaults_and_struct_size():
     """bsmr_plan_options_default fills exactly the ctypes mirror of the C struct."""
     n = ctypes.sizeof(bsmr.PlanOptions)

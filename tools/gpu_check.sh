@@ -19,7 +19,7 @@ bash tools/gpu_pmc.sh "pmc_$TAG" 128 &&
 python3 tools/pmc_traffic.py "$OUT/pmc_$TAG" profiles/traffic_C2_K128.json > "$OUT/traffic_$TAG.json" &&
 timeout -k 10 300 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o prof -- \
-    python3 bench.py --no-cpu-baseline --no-split > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
+    python3 bench.py --no-cpu-baseline --no-vendor --no-split > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
 rc=$?
 echo "gpu_check rc=$rc" > "$OUT/gpu_check_$TAG.rc"
 exit $rc

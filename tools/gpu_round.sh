@@ -14,7 +14,7 @@ step pmc && bash tools/gpu_pmc.sh "$TAG/pmc" 128 &&
 python3 tools/pmc_traffic.py "$OUT/pmc" profiles/traffic_C2_K128.json > "$OUT/traffic_C2_K128.json" &&
 step bench && timeout -k 10 300 python3 bench.py > "$OUT/bench_C2.json" 2> "$OUT/bench_C2.err" &&
 step rocprof && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o prof -- \
-    python3 bench.py --no-cpu-baseline --no-split > "$OUT/bench_C2_rocprof.json" 2> "$OUT/bench_C2_rocprof.err" &&
+    python3 bench.py --no-cpu-baseline --no-vendor --no-split > "$OUT/bench_C2_rocprof.json" 2> "$OUT/bench_C2_rocprof.err" &&
 step C3 && timeout -k 10 600 python3 bench.py --config C3 --steps 50 --warmup 5 > "$OUT/bench_C3.json" 2> "$OUT/bench_C3.err" &&
 step C5u && timeout -k 10 300 python3 bench.py --config C5 --mask uniform --steps 100 --warmup 10 > "$OUT/bench_C5u.json" 2> "$OUT/bench_C5u.err" &&
 step C5b && timeout -k 10 300 python3 bench.py --config C5 --mask block --steps 100 --warmup 10 > "$OUT/bench_C5b.json" 2> "$OUT/bench_C5b.err" &&

@@ -23,13 +23,15 @@ def main():
     ap.add_argument("--layout", default="auto", choices=["auto", "rowblock", "colmajor"])
     ap.add_argument("--lds-kb", type=int, default=0)
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
+    ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
     args = ap.parse_args()
     import torch
 
     import bsmr
     from bsmr import Plan, make_data, synth
 
-    M, N, rp, ci = getattr(synth, args.workload)()
+    gen = getattr(synth, args.workload)
+    M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
     K = args.K
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout,
                 lds_budget_kb=args.lds_kb)
