@@ -24,7 +24,10 @@ def main():
     ap.add_argument("--lds-kb", type=int, default=0)
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
+    ap.add_argument("--diag", type=int, default=0, help="BSMR_DIAG ablation bits (sddmm.hip)")
     args = ap.parse_args()
+    if args.diag:
+        os.environ["BSMR_DIAG"] = str(args.diag)
     import torch
 
     import bsmr
