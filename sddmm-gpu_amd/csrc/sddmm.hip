@@ -616,8 +616,7 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             for (u32 h = 0; h < NC; h += H) {
                 f32x4 av[H];
 #pragma unroll
-                for (u32 f = 0; f < H; ++f)
-                    av[f] = (a.diag & 512) ? bv[h + f] : ld16(As + (ab + rot[h + f]));  // 512: no LDS
+                for (u32 f = 0; f < H; ++f) av[f] = ld16(As + (ab + rot[h + f]));
 #pragma unroll
                 for (u32 f = 0; f < H; ++f) chunk_dot<DT>(av[f], bv[h + f], acc0, acc1);
             }
@@ -629,8 +628,7 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             if constexpr (G == 16) sm += dppf<0x140>(sm);  // row_mirror: the other half-row
             if (sub == static_cast<u32>(i)) res = sm;
         }
-        // diag 256: store only an impossible value (keeps the math, drops the P scatter)
-        if (sub < nb && (!(a.diag & 256) || res == -1234.5f)) a.P[pc.mo[k]] = res;
+        if (sub < nb) a.P[pc.mo[k]] = res;
     }
 }
 
@@ -658,7 +656,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
     // staging loads so all of it is in flight together
     const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
-    u32 np = (a.mode & 2) ? pend - it.w : 0u;
+    const u32 np = (a.mode & 2) ? pend - it.w : 0u;
     const u32 gr = tid / G;
     u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
 #pragma unroll
@@ -720,9 +718,8 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         pn.len = 0;
         if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
     };
-    if (a.diag & 64) np = 0;  // ablation: no residual compute (phase-0 pieces still loaded)
     if (NG < np) fetch(1);
-    if (pc.len && np) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     for (u32 ph = 1; ph * NG < np; ++ph) {
         pc = pn;
 #pragma unroll
