@@ -66,6 +66,9 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     p.force_rowblock = o.layout == BSMR_LAYOUT_ROWBLOCK;
     if (o.lds_budget_kb) p.rb_lds_kb = o.lds_budget_kb;
     if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
+    if (const char* po = std::getenv("BSMR_PIECE_ORDER")) p.piece_order = static_cast<u32>(std::atoi(po));
+    if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
+        p.l2_range_kb = std::max(64, std::atoi(l2));
     u64 free_mem = o.free_mem_bytes;
     if (free_mem == 0) {
         size_t fr = 0, tot = 0;

@@ -698,18 +698,21 @@ __global__ void k_cm_gather(const u32* __restrict__ order, const u32* __restrict
 }
 
 // Row-block layout: key = rowblock(q) * N + col (u64), q = reordered position of the entry's row.
+// Panel range [pa, pa + gridDim.x): entry e is stored at i = e - sdoff[pa], q relative to 16 pa.
 __global__ __launch_bounds__(256) void k_rb_keys(const u32* __restrict__ sdoff,
                                                  const u32* __restrict__ sparseRel,
-                                                 const u32* __restrict__ sparseColIdx, u32 RB,
-                                                 u32 N, unsigned long long* __restrict__ keys,
+                                                 const u32* __restrict__ sparseColIdx, u32 pa,
+                                                 u32 RB, u32 N,
+                                                 unsigned long long* __restrict__ keys,
                                                  u32* __restrict__ vals, u32* __restrict__ qOf) {
-    const u32 p = blockIdx.x;
+    const u32 p = pa + blockIdx.x;
+    const u32 base = sdoff[pa];
     const u32 e0 = sdoff[p], e1 = sdoff[p + 1];
     for (u32 e = e0 + threadIdx.x; e < e1; e += 256) {
-        const u32 q = p * 16 + sparseRel[e];
-        keys[e] = static_cast<unsigned long long>(q / RB) * N + sparseColIdx[e];
-        vals[e] = e;
-        qOf[e] = q;
+        const u32 q = blockIdx.x * 16 + sparseRel[e];
+        keys[e - base] = static_cast<unsigned long long>(q / RB) * N + sparseColIdx[e];
+        vals[e - base] = e - base;
+        qOf[e - base] = q;
     }
 }
 
@@ -839,16 +842,36 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
 }
 }  // namespace
 
-int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
-    RowBlockLayout& L = rbl[slot];
+const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, u32 pa, u32 pb, int* err) const {
+    *err = BSMR_OK;
+    if (pa == 0 && pb == P) {
+        const int slot = rowBytes == 256 ? 0 : rowBytes == 512 ? 1 : rowBytes == 1024 ? 2 : 3;
+        RowBlockLayout& L = rbl[slot];
+        if (L.rowBytes != rowBytes) *err = build_rowblock_layout(L, rowBytes, 0, P);
+        return *err == BSMR_OK ? &L : nullptr;
+    }
+    for (const auto& L : shard_rbl)
+        if (L->rowBytes == rowBytes && L->pa == pa && L->pb == pb) return L.get();
+    auto L = std::make_unique<RowBlockLayout>();
+    *err = build_rowblock_layout(*L, rowBytes, pa, pb);
+    if (*err != BSMR_OK) return nullptr;
+    if (shard_rbl.size() >= MAX_SHARD_LAYOUTS) shard_rbl.erase(shard_rbl.begin());
+    shard_rbl.push_back(std::move(L));
+    return shard_rbl.back().get();
+}
+
+// Row-block launch layout over panels [pa, pb) (the whole plan, or one row-panel shard).
+int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb) const {
     L.rowBytes = 0;
     hipStream_t s = stream;
     if (N > (1u << 22)) {
         set_error("row-block layout needs N <= 2^22");
         return BSMR_ERR_UNSUPPORTED;
     }
-    const u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, R);
-    const u32 nRB = (R + RBr - 1) / RBr;
+    const u32 qa = 16 * pa, qend = std::min(R, 16 * pb);
+    const u32 Rs = qend > qa ? qend - qa : 0;  // reordered rows of the range
+    const u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, Rs);
+    const u32 nRB = std::max<u32>(1, (Rs + RBr - 1) / RBr);
     const size_t lds = static_cast<size_t>(RBr) * rowBytes;
     const u32 NT = lds > 80 * 1024 ? 1024 : 512;
     const u32 wgPerCU = std::max<u32>(1, std::min<u32>(static_cast<u32>(160 * 1024 / lds), 2048 / NT));
@@ -856,7 +879,8 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
     const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
-    const u32 n = nres;
+    const u32 ebase = h_sparseValueOffsets[pa];
+    const u32 n = h_sparseValueOffsets[pb] - ebase;
     BSMR_CHECK(L.meta.alloc(std::max<u32>(n, 1)));
     BSMR_CHECK(L.out.alloc(std::max<u32>(n, 1)));
     std::vector<u32> rbEnd(nRB, 0), hmeta(n);
@@ -870,13 +894,13 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
         BSMR_CHECK(qOf.alloc(n));
         BSMR_CHECK(dEnd.alloc(nRB));
         BSMR_HIP(hipMemsetAsync(dEnd.data(), 0, nRB * sizeof(u32), s));
-        hipLaunchKernelGGL(k_rb_keys, dim3(P), dim3(256), 0, s, sparseValueOffsets.data(),
-                           sparseRel.data(), sparseColIdx.data(), RBr, N, keys.data(), vals.data(),
-                           qOf.data());
+        hipLaunchKernelGGL(k_rb_keys, dim3(pb - pa), dim3(256), 0, s, sparseValueOffsets.data(),
+                           sparseRel.data(), sparseColIdx.data(), pa, RBr, N, keys.data(),
+                           vals.data(), qOf.data());
         BSMR_CHECK(sort_pairs64(keys.data(), skeys.data(), vals.data(), order.data(), n,
                                 bits_for(static_cast<u64>(nRB) * N), tmp, s));
         hipLaunchKernelGGL(k_rb_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
-                           qOf.data(), sparseColIdx.data(), sparseValues.data(), n, RBr,
+                           qOf.data(), sparseColIdx.data() + ebase, sparseValues.data() + ebase, n, RBr,
                            L.meta.data(), L.out.data(), dEnd.data());
         BSMR_HIP(hipGetLastError());
         BSMR_HIP(hipMemcpyAsync(rbEnd.data(), dEnd.data(), nRB * sizeof(u32), hipMemcpyDeviceToHost, s));
@@ -884,70 +908,97 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
         BSMR_HIP(hipStreamSynchronize(s));
         for (u32 b = 1; b < nRB; ++b) rbEnd[b] = std::max(rbEnd[b], rbEnd[b - 1]);
     }
-    // column cuts: XCD_BUCKETS ranges of (nearly) equal residual count
+    // column ranges: NCR = 8 m ranges of (nearly) equal residual count; XCD x owns ranges
+    // [x m, (x + 1) m). m makes one range's B columns (N rowBytes / NCR) fit an L2 budget: the
+    // items of an XCD are ordered by range, so the B columns an item gathers were brought into
+    // that XCD's L2 by the items before it (graph matrices: B is gathered once per row block and
+    // column run, from L2 instead of the Infinity Cache)
     constexpr u32 CM = (1u << 22) - 1;
-    std::vector<u32> cuts(XCD_BUCKETS + 1, N);
+    const u32 m = std::max<u32>(1, static_cast<u32>(std::ceil(
+        static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(l2_range_kb) * 1024.0))));
+    const u32 NCR = XCD_BUCKETS * m;
+    std::vector<u32> cuts(NCR + 1, N);
     cuts[0] = 0;
     {
         std::vector<u32> cnt(N + 1, 0);
         for (u32 i = 0; i < n; ++i) ++cnt[hmeta[i] & CM];
         u64 run = 0;
         u32 x = 1;
-        for (u32 c = 0; c < N && x < XCD_BUCKETS; ++c) {
-            while (x < XCD_BUCKETS && run >= static_cast<u64>(n) * x / XCD_BUCKETS) cuts[x++] = c;
+        for (u32 c = 0; c < N && x < NCR; ++c) {
+            while (x < NCR && run >= static_cast<u64>(n) * x / NCR) cuts[x++] = c;
             run += cnt[c];
         }
-        for (; x < XCD_BUCKETS; ++x) cuts[x] = N;
+        for (; x < NCR; ++x) cuts[x] = N;
     }
-    // segments (rb, bucket): entries of rb in the bucket's column range + 1/8 of rb's tiles
-    const u32 nseg = nRB * XCD_BUCKETS;
-    std::vector<u32> se0(nseg), se1(nseg), st0(nseg), st1(nseg);
+    // segments (rb, range k): entries of rb in range k + 1/NCR of rb's tiles; cost = entries +
+    // column-run pieces (one B column each) + 16 per tile
+    const size_t nseg = static_cast<size_t>(nRB) * NCR;
+    std::vector<u32> se0(nseg), se1(nseg), st0(nseg), st1(nseg), spc(nseg, 0);
     std::vector<double> cost(nseg);
+    std::vector<u64> piecesRB(nRB, 0);
     for (u32 b = 0; b < nRB; ++b) {
         const u32 eb0 = b ? rbEnd[b - 1] : 0, eb1 = rbEnd[b];
-        const u32 p0 = std::min(b * (RBr / 16), P), p1 = std::min((b + 1) * (RBr / 16), P);
+        const u32 p0 = std::min(pa + b * (RBr / 16), pb), p1 = std::min(pa + (b + 1) * (RBr / 16), pb);
         const u32 t0 = h_blockOffsets[p0], nt = h_blockOffsets[p1] - t0;
-        for (u32 x = 0; x < XCD_BUCKETS; ++x) {
-            const u32 i = b * XCD_BUCKETS + x;
-            auto lb = [&](u32 col) {
-                return static_cast<u32>(std::lower_bound(hmeta.begin() + eb0, hmeta.begin() + eb1, col,
-                                                         [](u32 m, u32 c) { return (m & CM) < c; }) -
-                                        hmeta.begin());
-            };
-            se0[i] = x ? lb(cuts[x]) : eb0;
-            se1[i] = x + 1 < XCD_BUCKETS ? lb(cuts[x + 1]) : eb1;
-            st0[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * x / XCD_BUCKETS);
-            st1[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * (x + 1) / XCD_BUCKETS);
-            cost[i] = (se1[i] - se0[i]) + 16.0 * (st1[i] - st0[i]);
+        u32 lo = eb0;
+        for (u32 k = 0; k < NCR; ++k) {
+            const size_t i = static_cast<size_t>(b) * NCR + k;
+            const u32 hi = k + 1 < NCR
+                               ? static_cast<u32>(std::lower_bound(hmeta.begin() + lo, hmeta.begin() + eb1,
+                                                                   cuts[k + 1],
+                                                                   [](u32 v, u32 c) { return (v & CM) < c; }) -
+                                                  hmeta.begin())
+                               : eb1;
+            se0[i] = lo;
+            se1[i] = hi;
+            for (u32 e = lo; e < hi;) {  // column runs cut every RB_PIECE_MAX entries
+                const u32 col = hmeta[e] & CM;
+                u32 f = e + 1;
+                while (f < hi && f - e < RB_PIECE_MAX && (hmeta[f] & CM) == col) ++f;
+                ++spc[i];
+                e = f;
+            }
+            piecesRB[b] += spc[i];
+            lo = hi;
+            st0[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * k / NCR);
+            st1[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * (k + 1) / NCR);
+            cost[i] = (se1[i] - se0[i]) + spc[i] + 16.0 * (st1[i] - st0[i]);
         }
     }
-    // chunks: one round of workgroup slots (Q items) unless items would drop below ~128 units. A
-    // row block big enough for >= 8 items is split by the XCD column ranges (its items then read B
-    // from their own XCD's L2); a smaller one (e.g. banded matrices: many row blocks of few
-    // entries) is cut along its whole column-sorted entry list, and its items balance the XCD list
-    // lengths. Item counts come from largest-remainder apportionment, so one round of slots is
-    // not exceeded unless there are more row blocks than slots.
+    // chunks. A row block is split by the column ranges (its items then read B from their own
+    // XCD's L2) when it is big enough for >= 8 items of a one-round launch, or (m > 1) when its
+    // column runs would gather more B rows than NCR restagings of its A rows cost; a smaller one
+    // (e.g. banded matrices: many row blocks of few entries) is cut along its whole column-sorted
+    // entry list, and its items balance the XCD list lengths. Item counts come from
+    // largest-remainder apportionment; Q is one round of workgroup slots (fewer if items would
+    // drop below ~128 cost units), or whole rounds when the split segments need more items.
     std::vector<std::vector<uint4>> lists(XCD_BUCKETS);
     std::vector<std::vector<u32>> lends(XCD_BUCKETS);
     double total = 0;
     for (double c : cost) total += c;
-    // an item is worth its row-block staging from ~128 cost units (entries; a tile counts 16)
-    const u32 Q = std::max<u32>(1, std::min<u32>(perBucket * XCD_BUCKETS, static_cast<u32>(total / 128.0)));
+    const u32 Q1 = perBucket * XCD_BUCKETS;
+    u32 Q = std::max<u32>(1, std::min<u32>(Q1, static_cast<u32>(total / 128.0)));
     const double target = total / Q;
     std::vector<double> cb(nRB, 0.0);
     std::vector<char> split(nRB, 0);
     double splitTotal = 0;
+    std::vector<u32> segX(XCD_BUCKETS, 0);  // non-empty split segments per XCD
     for (u32 b = 0; b < nRB; ++b) {
-        for (u32 x = 0; x < XCD_BUCKETS; ++x) cb[b] += cost[b * XCD_BUCKETS + x];
-        split[b] = cb[b] >= XCD_BUCKETS * target;
-        if (split[b]) splitTotal += cb[b];
+        for (u32 k = 0; k < NCR; ++k) cb[b] += cost[static_cast<size_t>(b) * NCR + k];
+        split[b] = cb[b] >= XCD_BUCKETS * target ||
+                   (m > 1 && piecesRB[b] >= static_cast<u64>(NCR) * RBr);
+        if (!split[b]) continue;
+        splitTotal += cb[b];
+        for (u32 k = 0; k < NCR; ++k)
+            segX[k / m] += cost[static_cast<size_t>(b) * NCR + k] > 0;
     }
-    // the same quota for every bucket (the column cuts balance them): an extra item in one
-    // bucket would start a second round of slots on that XCD
-    const u32 qEach = static_cast<u32>(
-        std::llround(static_cast<double>(Q / XCD_BUCKETS) * (total > 0 ? splitTotal / total : 0.0)));
+    // the same quota for every XCD (the column cuts balance them): an extra item in one list
+    // would start another round of slots on that XCD
+    const u32 segMax = *std::max_element(segX.begin(), segX.end());
+    if (segMax * XCD_BUCKETS > Q) Q = (segMax * XCD_BUCKETS + Q1 - 1) / Q1 * Q1;
+    const u32 qEach = std::max<u32>(segMax, static_cast<u32>(std::llround(
+        static_cast<double>(Q / XCD_BUCKETS) * (total > 0 ? splitTotal / total : 0.0))));
     const u32 qSplit = qEach * XCD_BUCKETS;
-    const std::vector<u32> qx(XCD_BUCKETS, qEach);
     std::vector<double> cu(nRB, 0.0);
     for (u32 b = 0; b < nRB; ++b) cu[b] = split[b] ? 0.0 : cb[b];
     const std::vector<u32> nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u);
@@ -963,13 +1014,19 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
         }
     };
     for (u32 x = 0; x < XCD_BUCKETS; ++x) {
-        std::vector<double> c(nRB, 0.0);
-        for (u32 b = 0; b < nRB; ++b) c[b] = split[b] ? cost[b * XCD_BUCKETS + x] : 0.0;
-        const std::vector<u32> nch = apportion(c, qx[x]);
-        for (u32 b = 0; b < nRB; ++b) {
-            const u32 i = b * XCD_BUCKETS + x;
-            if (nch[b]) emit(x, b, se0[i], se1[i] - se0[i], st0[i], st1[i] - st0[i], nch[b]);
-        }
+        // XCD x's segments in (range, row block) order
+        std::vector<double> c(static_cast<size_t>(m) * nRB, 0.0);
+        for (u32 j = 0; j < m; ++j)
+            for (u32 b = 0; b < nRB; ++b)
+                c[static_cast<size_t>(j) * nRB + b] =
+                    split[b] ? cost[static_cast<size_t>(b) * NCR + x * m + j] : 0.0;
+        const std::vector<u32> nch = apportion(c, qEach);
+        for (u32 j = 0; j < m; ++j)
+            for (u32 b = 0; b < nRB; ++b) {
+                const size_t i = static_cast<size_t>(b) * NCR + x * m + j;
+                const u32 q = nch[static_cast<size_t>(j) * nRB + b];
+                if (q) emit(x, b, se0[i], se1[i] - se0[i], st0[i], st1[i] - st0[i], q);
+            }
     }
     // unsplit row blocks: their items, in row-block order, go to the list with the fewest items,
     // so no XCD runs an extra round (a contiguous range of blocks per XCD, for L2 sharing of
@@ -979,7 +1036,7 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
     lends.resize(XCD_BUCKETS + 1);
     for (u32 b = 0; b < nRB; ++b) {
         if (!nu[b]) continue;
-        const u32 i0 = b * XCD_BUCKETS, i1 = i0 + XCD_BUCKETS - 1;
+        const size_t i0 = static_cast<size_t>(b) * NCR, i1 = i0 + NCR - 1;
         emit(spare, b, se0[i0], se1[i1] - se0[i0], st0[i0], st1[i1] - st0[i0], nu[b]);
     }
     {
@@ -1003,8 +1060,13 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
             ends[j * XCD_BUCKETS + x] = lends[x][j];
         }
     // column-run pieces: each item's entries [e0, e1) cut at column changes and every
-    // RB_PIECE_MAX entries; piece {first entry, column | (length - 1) << 22}, longest first so
-    // the 16 row-groups of a wave get pieces of similar length
+    // RB_PIECE_MAX entries; piece {first entry, column | (length - 1) << 22}. A workgroup's NG
+    // row-groups take one piece each per phase, so phase ph runs the item's pieces
+    // [ph NG, (ph + 1) NG). Longest first, so the 16 row-groups of a wave get pieces of similar
+    // length: over the whole item (piece_order 0), or inside column windows of one phase
+    // (piece_order 1: all items of an XCD would sweep their column range together)
+    const u32 G = rowBytes >= 2048 ? 16 : rowBytes >= 1024 ? 8 : 4;  // sddmm.hip RowGeom
+    const u32 NG = piece_order == 1 ? NT / G : 0xFFFFFFFFu;  // sort window
     std::vector<uint2> pieces;
     pieces.reserve(n / 4 + items.size());
     std::vector<uint2> mine;
@@ -1018,8 +1080,9 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
             mine.push_back(make_uint2(e, col | ((f - e - 1) << 22)));
             e = f;
         }
-        std::stable_sort(mine.begin(), mine.end(),
-                         [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
+        for (size_t w0 = 0; w0 < mine.size(); w0 += NG)
+            std::stable_sort(mine.begin() + w0, mine.begin() + std::min<size_t>(mine.size(), w0 + NG),
+                             [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
         items[i].w = static_cast<u32>(pieces.size());
         pieces.insert(pieces.end(), mine.begin(), mine.end());
         ends[i] = static_cast<u32>(pieces.size());
@@ -1034,6 +1097,9 @@ int Plan::build_rowblock_layout(int slot, u32 rowBytes) const {
     L.NT = NT;
     L.lds = lds;
     L.nRB = nRB;
+    L.pa = pa;
+    L.pb = pb;
+    L.rowEnd = qend;
     L.rowBytes = rowBytes;
     return BSMR_OK;
 }
@@ -1206,6 +1272,7 @@ int Plan::build_columns() {
         segments_ready = true;
     }
     for (auto& L : rbl) L.rowBytes = 0;  // launch layouts depend on the column split
+    shard_rbl.clear();
     // pass 1
     const u32 thr =static_cast<u32>(std::ceil(delta * static_cast<float>(TILE)));  // colReordering.cu:246
     DevBuf<u32> phist, pnd, pns, psd;

@@ -1,6 +1,7 @@
 // plan.hpp — the device-resident BSMR plan (reference BSMR + RPHM, include/BSMR.hpp:21-159).
 #pragma once
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -37,6 +38,11 @@ struct Plan {
     bool force_rowblock = false;  // BSMR_LAYOUT_ROWBLOCK: also for tile-dominated plans
     u32 rb_lds_kb = 144;  // LDS budget of a row-block workgroup (bsmr_plan_options.lds_budget_kb)
     u32 diag = 0;  // BSMR_DIAG profiling ablations (wrong results; never set in normal use)
+    // row-block piece order inside an item (tuning experiments: BSMR_PIECE_ORDER): 0 = longest
+    // first over the whole item, 1 = column windows of one phase, longest first inside
+    u32 piece_order = 0;
+    // L2 budget of one column range of the row-block layout (KiB; BSMR_L2_RANGE_KB)
+    u32 l2_range_kb = 2048;
     u32 cluster_batch = 512;
 
     // input
@@ -80,6 +86,9 @@ struct Plan {
     // column in the same (full-width) instruction. items[i].w / itemEnd[i] delimit its pieces.
     struct RowBlockLayout {
         u32 rowBytes = 0, RB = 0, NT = 1024, nRB = 0, nItems = 0, nPieces = 0;
+        // panels [pa, pb) covered (the whole plan: 0, P); row block b starts at reordered
+        // position 16 * pa + b * RB; rows at or past rowEnd = min(R, 16 * pb) are not staged
+        u32 pa = 0, pb = 0, rowEnd = 0;
         size_t lds = 0;
         DevBuf<u32> meta;   // local row << 22 | column
         DevBuf<u32> out;    // output index (CSR position)
@@ -89,7 +98,12 @@ struct Plan {
     };
     static constexpr int N_RB_LAYOUTS = 4;  // rows of 256, 512, 1024 and 2048 bytes
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
-    int build_rowblock_layout(int slot, u32 rowBytes) const;
+    // layouts of panel ranges (row-panel shards, bsmr_sddmm_panels), most recent last
+    static constexpr size_t MAX_SHARD_LAYOUTS = 16;
+    mutable std::vector<std::unique_ptr<RowBlockLayout>> shard_rbl;
+    int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb) const;
+    // the (cached) layout for rows of rowBytes over panels [pa, pb); null on error
+    const RowBlockLayout* rowblock_layout(u32 rowBytes, u32 pa, u32 pb, int* err) const;
 
     mutable DevBuf<uint8_t> tmp;  // scan/sort scratch
     // BSMR_DIAG & 32 debug timeline (4 u64 per wave of the last launch)

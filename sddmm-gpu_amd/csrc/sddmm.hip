@@ -397,7 +397,8 @@ struct RbArgs {
     const char* B;  // N rows of K elements (B column-major)
     float* P;
     const u32* rows;
-    u32 R, N, RB;
+    u32 R, N, RB;  // R: rows at or past this reordered position are not staged (range end)
+    u32 qbase;     // reordered position of row block 0 (16 * first panel of the range)
     const uint4* items;     // {row block, tile begin, tile end, piece begin}
     const u32* itemEnd;     // piece end
     const uint2* pieces;    // {first entry, column | (length - 1) << 22}
@@ -650,7 +651,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     const uint4 it = a.items[blockIdx.x];
     const u32 pend = a.itemEnd[blockIdx.x];
     if (it.y == it.z && it.w == pend) return;  // padding item (uniform across the workgroup)
-    const u32 q0 = it.x * a.RB;
+    const u32 q0 = a.qbase + it.x * a.RB;
     const u32 tid = threadIdx.x, w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
     // every wave takes (at most) one dense tile and its row-groups one residual piece each per
     // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
@@ -708,13 +709,15 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     }
     if (tw < ntile) dt.run(a, As, tb);
     const unsigned long long td = rtime(a.trace);
-    // later phases (items with more pieces than row-groups, e.g. short column runs): the extra
-    // pieces are the shortest and go to the groups that had the shortest phase-0 pieces; phase
-    // ph's piece and B column are loaded while phase ph - 1 computes (two register sets)
+    // later phases (items with more pieces than row-groups, e.g. short column runs): phase ph
+    // runs the column window [ph NG, (ph + 1) NG) of the item's pieces (longest first inside;
+    // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
+    // alternates long and short pieces; phase ph's piece and B column are loaded while phase
+    // ph - 1 computes (two register sets)
     Piece<RBY> pn;
     f32x4 nb[NC];
     auto fetch = [&](const u32 ph) {
-        const u32 pi = ph * NG + (NG - 1 - gr);
+        const u32 pi = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
         pn.len = 0;
         if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
     };
@@ -812,24 +815,25 @@ int rb_slot(const Plan& p, u32 K, int dtype) {
     return rby == 256 ? 0 : rby == 512 ? 1 : rby == 1024 ? 2 : rby == 2048 ? 3 : -1;
 }
 
-int ensure_rb_layout(const Plan& p, int slot) {
+// the row-block layout of panels [pa, pb) for slot's row size (built on first use)
+int get_rb_layout(const Plan& p, int slot, u32 pa, u32 pb, const Plan::RowBlockLayout** out) {
     std::lock_guard<std::mutex> g(p.layout_mu);
-    const u32 rby = 256u << slot;
-    if (p.rbl[slot].rowBytes == rby) return BSMR_OK;
-    return p.build_rowblock_layout(slot, rby);
+    int err = BSMR_OK;
+    *out = p.rowblock_layout(256u << slot, pa, pb, &err);
+    return err;
 }
 
 // mode: 1 = dense tiles only, 2 = residual only, 3 = both (profiling splits)
-int launch_rb(const Plan& p, int slot, const void* dA, const void* dB, float* dP, int dtype,
-              u32 mode, hipStream_t s, u32 nb = 1) {
-    const Plan::RowBlockLayout& L = p.rbl[slot];
+int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, const void* dB,
+              float* dP, int dtype, u32 mode, hipStream_t s, u32 nb = 1) {
     if (L.nItems == 0) return BSMR_OK;
     RbArgs a{};
     a.A = static_cast<const char*>(dA);
     a.B = static_cast<const char*>(dB);
     a.P = dP;
     a.rows = p.rows.data();
-    a.R = p.R;
+    a.R = L.rowEnd;
+    a.qbase = 16 * L.pa;
     a.N = p.N;
     a.RB = L.RB;
     a.items = L.items.data();
@@ -920,8 +924,9 @@ extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const
         float* P = dP + static_cast<size_t>(b0) * p.nnz;
         const int slot = rb_slot(p, K, dtype);
         if (slot >= 0) {
-            BSMR_CHECK(ensure_rb_layout(p, slot));
-            BSMR_CHECK(launch_rb(p, slot, A, B, P, dtype, 3, s, nb));
+            const Plan::RowBlockLayout* L = nullptr;
+            BSMR_CHECK(get_rb_layout(p, slot, 0, p.P, &L));
+            BSMR_CHECK(launch_rb(p, *L, A, B, P, dtype, 3, s, nb));
             continue;
         }
         if (dtype != BSMR_F32) {
@@ -950,13 +955,22 @@ extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const vo
     }
     const Plan& p = plan->p;
     BSMR_CHECK(validate(dA, dB, K, dtype, dP));
-    if (dtype != BSMR_F32) {
-        set_error("bsmr_sddmm_panels: panel ranges support fp32 A/B only");
-        return BSMR_ERR_UNSUPPORTED;
-    }
     if (p0 > p1 || p1 > p.P) {
         set_error("bsmr_sddmm_panels: bad panel range");
         return BSMR_ERR_INVALID;
+    }
+    if (p0 == p1) return BSMR_OK;
+    // the row-block kernel over the range's own layout (same kernel as the whole plan)
+    const int slot = rb_slot(p, K, dtype);
+    if (slot >= 0) {
+        const Plan::RowBlockLayout* L = nullptr;
+        BSMR_CHECK(get_rb_layout(p, slot, p0, p1, &L));
+        return launch_rb(p, *L, dA, dB, dP, dtype, 3, static_cast<hipStream_t>(stream));
+    }
+    if (dtype != BSMR_F32) {
+        set_error("bsmr_sddmm_panels: fp16/bf16 panel ranges need the row-block layout "
+                  "(half K in 128..1024)");
+        return BSMR_ERR_UNSUPPORTED;
     }
     // items are stored panel-major: ceil(tiles_q / TILES_PER_ITEM) dense and
     // ceil(nres_q / RES_PER_ITEM) residual items per panel q
@@ -994,7 +1008,8 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     hipEvent_t ev[4];
     for (auto& e : ev) BSMR_HIP(hipEventCreate(&e));
     const int slot = rb_slot(p, K, dtype);
-    if (slot >= 0) BSMR_CHECK(ensure_rb_layout(p, slot));
+    const Plan::RowBlockLayout* L = nullptr;
+    if (slot >= 0) BSMR_CHECK(get_rb_layout(p, slot, 0, p.P, &L));
     SddmmArgs full = make_args(p, dA, dB, K, dP);
     full.nd = p.nDenseItems;
     full.nslots = p.nSlots;
@@ -1003,7 +1018,7 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     SddmmArgs res = full;
     res.nd = 0;
     auto run = [&](u32 mode) -> int {
-        if (slot >= 0) return launch_rb(p, slot, dA, dB, dP, dtype, mode, s);
+        if (L) return launch_rb(p, *L, dA, dB, dP, dtype, mode, s);
         if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, mode, s);
         return launch_full(p, mode == 1 ? dense : mode == 2 ? res : full, s);
     };

@@ -14,7 +14,7 @@ import oracle_lib as O
 from bsmr import Plan, make_data, synth
 from golden_common import (ALPHAS, DELTAS, REF_FREE_MEM, compare, expected_from_stats, matrix,
                            record)
-from gpu_util import assert_plans_equal, oracle_plan, run_sddmm, torch_cuda
+from gpu_util import assert_plans_equal, half_values, oracle_plan, run_sddmm, torch_cuda
 
 pytestmark = pytest.mark.gpu
 
@@ -185,6 +185,32 @@ def test_panel_shards_cover_every_output(world):
     for r in rows[p0 * 16: p1 * 16]:
         mine[rp[r]:rp[r + 1]] = True
     assert np.isfinite(part[mine]).all() and np.isnan(part[~mine]).all()
+
+
+@pytest.mark.parametrize("K,dtype,world", [(128, 0, 4), (32, 0, 3), (256, 1, 5), (512, 2, 2),
+                                           (128, 0, 1)])
+def test_panel_shards_rowblock_kernel(K, dtype, world):
+    """Row-panel shards on the row-block kernel (a layout per panel range) for fp32/fp16/bf16,
+    and the column-major fallback (fp32 K=32): every output written once, by its own shard."""
+    M, N, rp, ci = small_cases()["zipf"]
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    shards = [plan.shard(K, r, world) for r in range(world)]
+    A = make_data(M * K)
+    B = make_data(N * K)
+    P = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
+    if dtype:
+        A, B = half_values(A, dtype), half_values(B, dtype)
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
+    assert np.isfinite(P).all()
+    assert O.check_data(ref, P) == 0
+    rows = plan.array("reorderedRows")
+    for p0, p1 in shards:
+        part = run_sddmm(plan, A, B, K, len(ci), panels=[(p0, p1)], dtype=dtype)
+        mine = np.zeros(len(ci), bool)
+        for r in rows[p0 * 16: p1 * 16]:
+            mine[rp[r]:rp[r + 1]] = True
+        assert np.isfinite(part[mine]).all() and np.isnan(part[~mine]).all(), (p0, p1)
+        assert O.check_data(ref[mine], part[mine]) == 0
 
 
 def test_values_independent_of_layout_permutation():

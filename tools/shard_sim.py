@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Row-panel sharding rehearsal on ONE GPU: one global BSMR plan, the cost-model
+panel cuts for world = 1, 2, 4, 8, and each shard's SDDMM (bsmr_sddmm_panels: the row-block kernel
+over that shard's own layout) timed alone on the whole GPU with HIP events, as rank r of an N-GPU
+node would run it. Reports per-shard ms, the slowest shard (the job's step time), the imbalance
+(max / mean) and the aggregate GFLOP/s = 2 nnz K / slowest; checks the union of the shards against
+the unsharded launch (checkData rule). B broadcast time is not included (bench.py --gpus N
+measures it over RCCL).
+
+    python3 tools/shard_sim.py --workload reddit_like --scale 0.5 --K 128
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sddmm-gpu_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="reddit_like")
+    ap.add_argument("--scale", type=float, default=None)
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import bsmr
+    import oracle_lib as O
+    from bsmr import Plan, make_data, synth
+
+    gen = getattr(synth, args.workload)
+    M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
+    K = args.K
+    code = {"f32": bsmr.F32, "f16": bsmr.F16, "bf16": bsmr.BF16}[args.dtype]
+    tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
+    t0 = time.perf_counter()
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3)
+    plan_s = time.perf_counter() - t0
+    print(f"plan {plan_s:.1f} s", file=sys.stderr, flush=True)
+    nnz = len(ci)
+    dA = torch.from_numpy(make_data(M * K)).cuda().to(tdt)
+    dB = torch.from_numpy(make_data(N * K)).cuda().to(tdt)
+    dP = torch.zeros(nnz, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    s = stream.cuda_stream
+    flops = 2.0 * nnz * K
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.iters):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.iters
+
+    full_ms = timed(lambda: plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s,
+                                       dtype=code))
+    P_full = dP.cpu().numpy()
+    out = {"workload": args.workload, "scale": args.scale, "M": M, "N": N, "nnz": nnz, "K": K,
+           "dtype": args.dtype, "plan_build_s": round(plan_s, 2),
+           "unsharded": {"ms": round(full_ms, 5), "GFLOP/s": round(flops / full_ms / 1e6, 1)},
+           "worlds": {}}
+    bo = plan.array("blockOffsets").astype(np.int64)
+    so = plan.array("sparseValueOffsets").astype(np.int64)
+    for world in [int(w) for w in args.worlds.split(",")]:
+        shards = [plan.shard(K, r, world) for r in range(world)]
+        dP.fill_(float("nan"))
+        ms = []
+        for p0, p1 in shards:
+            ms.append(timed(lambda: plan.sddmm_panels(dA.data_ptr(), dB.data_ptr(), K,
+                                                       dP.data_ptr(), p0, p1, stream=s,
+                                                       dtype=code)))
+        P = dP.cpu().numpy()
+        slow = max(ms)
+        out["worlds"][world] = {
+            "shards": shards, "shard_ms": [round(x, 5) for x in ms],
+            "shard_tiles": [int(bo[b] - bo[a]) for a, b in shards],
+            "shard_residual": [int(so[b] - so[a]) for a, b in shards],
+            "step_ms": round(slow, 5), "imbalance": round(slow / (sum(ms) / len(ms)), 3),
+            "aggregate_GFLOP/s": round(flops / slow / 1e6, 1),
+            "unwritten": int(np.isnan(P).sum()),
+            "checkData_errors_vs_unsharded": O.check_data(P_full, P)}
+        print(json.dumps({world: out["worlds"][world]}), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

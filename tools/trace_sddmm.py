@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--lds-kb", type=int, default=0)
     ap.add_argument("--dump", default="")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
+    ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
+    ap.add_argument("--waves-per-wg", type=int, default=16, help="NT / 64 of the traced launch")
     args = ap.parse_args()
     os.environ["BSMR_DIAG"] = str(int(os.environ.get("BSMR_DIAG", "0")) | 32)
     import torch
@@ -35,7 +37,8 @@ def main():
     import bsmr
     from bsmr import Plan, make_data, synth
 
-    M, N, rp, ci = getattr(synth, args.workload)()
+    gen = getattr(synth, args.workload)
+    M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
     K = args.K
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout, lds_budget_kb=args.lds_kb)
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
@@ -54,7 +57,9 @@ def main():
     buf = np.zeros(n.value, np.uint64)
     L.bsmr_debug_trace(plan.h, buf.ctypes.data, C.byref(n))
     t = buf.reshape(-1, 4)
-    t = t[t[:, 2] > 0]
+    slot = np.arange(len(t))
+    keep = t[:, 2] > 0
+    t, slot = t[keep], slot[keep]
     if args.dump:
         np.save(args.dump, t)
     t0, tm, t1 = (t[:, i].astype(np.int64) for i in range(3))
@@ -69,7 +74,9 @@ def main():
            "start_us": pct((t0 - base) * us), "life_us": pct((t1 - t0) * us),
            "mid_us": pct((tm - t0) * us), "dense_us": pct((td - tm) * us),
            "tail_us": pct((t1 - td) * us), "end_us": pct((t1 - base) * us),
-           "per_xcd": {}}
+           "per_xcd": {},
+           # workgroup b = slot // waves-per-wg; the layout assumes XCD = b % 8
+           "xcd_is_block_mod8": float(np.mean(xcc == (slot // args.waves_per_wg) % 8))}
     for x in range(8):
         m = xcc == x
         if m.any():
