@@ -173,11 +173,18 @@ int bsmr_sddmm(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K
 int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const void* dA, const void* dB,
                      uint32_t K, int dtype, float* dP, void* stream);
 
-/* Row-panel sharding for multi-GPU runs: contiguous panel ranges balanced by a
- * cost model; bsmr_sddmm_panels computes only the outputs of panels [p0, p1). */
+/* Row-panel sharding for multi-GPU runs: rank's contiguous panel range [p0, p1)
+ * of `world`; bsmr_sddmm_panels computes only the outputs of those panels (any dtype on the
+ * row-block launch). When (K, dtype) runs the row-block launch the cuts fall on its row-block
+ * boundaries, balanced by the layout's item costs (entries, column-run pieces, tiles, staged
+ * rows; builds the layout on first use); otherwise by the per-panel model of bsmr_shard_cuts.
+ * bsmr_plan_shard = bsmr_plan_shard_dtype(..., BSMR_F32, ...). */
 int bsmr_plan_shard(const bsmr_plan* plan, uint32_t K, int rank, int world, uint32_t* p0,
                     uint32_t* p1);
-/* The same cost model on host offset arrays (no device): cuts[world+1], cuts[0]=0, cuts[world]=P. */
+int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtype, int rank, int world,
+                          uint32_t* p0, uint32_t* p1);
+/* Per-panel cost model on host offset arrays (no device): cuts[world+1], cuts[0]=0,
+ * cuts[world]=P. */
 int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* sparseValueOffsets, uint32_t P,
                     uint32_t K, int world, uint32_t* cuts);
 int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,

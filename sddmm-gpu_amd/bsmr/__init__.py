@@ -84,7 +84,8 @@ EXPORTS = [
     "bsmr_csr_info", "bsmr_csr_rowptr", "bsmr_csr_colidx", "bsmr_csr_values", "bsmr_csr_free",
     "bsmr_make_data", "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
     "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
-    "bsmr_sddmm", "bsmr_sddmm_batch", "bsmr_plan_shard", "bsmr_shard_cuts", "bsmr_sddmm_panels",
+    "bsmr_sddmm", "bsmr_sddmm_batch", "bsmr_plan_shard", "bsmr_plan_shard_dtype",
+    "bsmr_shard_cuts", "bsmr_sddmm_panels",
     "bsmr_sddmm_profile",
 ]
 
@@ -134,6 +135,8 @@ def lib():
     L.bsmr_sddmm_batch.argtypes = [vp, C.c_uint32, vp, vp, C.c_uint32, C.c_int, vp, vp]
     L.bsmr_plan_shard.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_uint32),
                                   C.POINTER(C.c_uint32)]
+    L.bsmr_plan_shard_dtype.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                        C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.bsmr_shard_cuts.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_int, _u32p]
     L.bsmr_sddmm_panels.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
                                     C.c_uint32, vp]
@@ -277,10 +280,11 @@ class Plan:
         _check(lib().bsmr_sddmm_panels(self.h, dA, dB, K, dtype, dP, p0, p1, stream or None),
                "bsmr_sddmm_panels")
 
-    def shard(self, K, rank, world):
+    def shard(self, K, rank, world, dtype=F32):
+        """Panel range [p0, p1) of `rank` (bsmr_plan_shard_dtype)."""
         p0, p1 = C.c_uint32(), C.c_uint32()
-        _check(lib().bsmr_plan_shard(self.h, K, rank, world, C.byref(p0), C.byref(p1)),
-               "bsmr_plan_shard")
+        _check(lib().bsmr_plan_shard_dtype(self.h, K, dtype, rank, world, C.byref(p0),
+                                           C.byref(p1)), "bsmr_plan_shard_dtype")
         return p0.value, p1.value
 
     def profile(self, dA, dB, K, dP, iters=10, stream=0, dtype=F32):

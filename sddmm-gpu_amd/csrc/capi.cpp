@@ -67,6 +67,8 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     if (o.lds_budget_kb) p.rb_lds_kb = o.lds_budget_kb;
     if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
     if (const char* po = std::getenv("BSMR_PIECE_ORDER")) p.piece_order = static_cast<u32>(std::atoi(po));
+    if (const char* tm = std::getenv("BSMR_TILE_MIN_F32")) p.tile_min_f32 = static_cast<u32>(std::atoi(tm));
+    if (const char* tm = std::getenv("BSMR_TILE_MIN_HALF")) p.tile_min_half = static_cast<u32>(std::atoi(tm));
     if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
         p.l2_range_kb = std::max(64, std::atoi(l2));
     u64 free_mem = o.free_mem_bytes;
@@ -126,8 +128,8 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
     s->col_reorder_ms = p.col_ms;
     s->dense_items = p.nDenseItems;
     s->residual_items = p.nResItems;
-    for (int i = 0; i < Plan::N_RB_LAYOUTS && i < 4; ++i) {
-        const Plan::RowBlockLayout& L = p.rbl[i];
+    for (int i = 0; i < 4; ++i) {  // per row size: the fp32 layout, else the fp16/bf16 one
+        const Plan::RowBlockLayout& L = p.rbl[i].rowBytes ? p.rbl[i] : p.rbl[i + 4];
         s->rb_rows[i] = L.rowBytes ? L.RB : 0;
         s->rb_items[i] = L.rowBytes ? L.nItems : 0;
         s->rb_pieces[i] = L.rowBytes ? L.nPieces : 0;
@@ -271,14 +273,40 @@ extern "C" int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* spa
 
 extern "C" int bsmr_plan_shard(const bsmr_plan* plan, uint32_t K, int rank, int world,
                                uint32_t* p0, uint32_t* p1) {
-    if (!plan || world <= 0 || rank < 0 || rank >= world) {
+    return bsmr_plan_shard_dtype(plan, K, BSMR_F32, rank, world, p0, p1);
+}
+
+extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtype, int rank,
+                                     int world, uint32_t* p0, uint32_t* p1) {
+    if (!plan || world <= 0 || rank < 0 || rank >= world || !p0 || !p1 || K == 0 || K % 16 ||
+        (dtype != BSMR_F32 && dtype != BSMR_F16 && dtype != BSMR_BF16)) {
         set_error("bsmr_plan_shard: bad arguments");
         return BSMR_ERR_INVALID;
     }
     const Plan& p = plan->p;
     std::vector<u32> cuts(world + 1);
-    BSMR_CHECK(bsmr_shard_cuts(p.h_blockOffsets.data(), p.h_sparseValueOffsets.data(), p.P, K,
-                               world, cuts.data()));
+    // row-block launches: cut at row-block boundaries of the whole plan's layout by its measured
+    // item costs (entries, column-run pieces, tiles, staged rows), so each shard's own layout has
+    // the same row blocks; otherwise the per-panel model of bsmr_shard_cuts
+    const Plan::RowBlockLayout* L = nullptr;
+    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
+    if (L && L->nRB > 0) {
+        const u32 nRB = L->nRB, ppr = L->RB / 16;
+        std::vector<double> cum(nRB + 1ull, 0.0);
+        for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b];
+        cuts[0] = 0;
+        for (int r = 1; r < world; ++r) {
+            const double target = cum[nRB] * r / world;
+            // the boundary closest to the target
+            u32 b = static_cast<u32>(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+            if (b > 0 && target - cum[b - 1] < cum[std::min(b, nRB)] - target) --b;
+            cuts[r] = std::max(cuts[r - 1], std::min(b * ppr, p.P));
+        }
+        cuts[world] = p.P;
+    } else {
+        BSMR_CHECK(bsmr_shard_cuts(p.h_blockOffsets.data(), p.h_sparseValueOffsets.data(), p.P, K,
+                                   world, cuts.data()));
+    }
     *p0 = cuts[rank];
     *p1 = cuts[rank + 1];
     return BSMR_OK;

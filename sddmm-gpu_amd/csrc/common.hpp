@@ -67,7 +67,7 @@ struct DevBuf {
     }
     int upload(const T* h, size_t count, hipStream_t s) {
         BSMR_CHECK(alloc(count));
-        if (count) BSMR_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+        if (count && h) BSMR_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
         return BSMR_OK;
     }
     int download(std::vector<T>& h, hipStream_t s) const {

@@ -716,16 +716,63 @@ __global__ __launch_bounds__(256) void k_rb_keys(const u32* __restrict__ sdoff,
     }
 }
 
+// stored entries of tiles [t0, t0 + gridDim.x) (one 256-thread block per tile)
+__global__ __launch_bounds__(256) void k_tile_nnz(const u32* __restrict__ blockValues, u32 t0,
+                                                  u32* __restrict__ cnt) {
+    __shared__ u32 wsum[4];
+    const u32 t = t0 + blockIdx.x;
+    const bool v = blockValues[static_cast<size_t>(t) * TILE + threadIdx.x] != NULLV;
+    const u64 m = __ballot(v);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// entries of the demoted tiles (doff[i] != NULLV: their first slot among the demoted entries)
+// become residual-style entries n0 + doff[i] + k in slot order: q relative to qa, column, output
+__global__ __launch_bounds__(256) void k_tile_demote(const u32* __restrict__ blockValues,
+                                                     const uint4* __restrict__ tilePanel,
+                                                     const u32* __restrict__ denseCols, u32 t0,
+                                                     const u32* __restrict__ doff, u32 qa, u32 RB,
+                                                     u32 N, u32 n0,
+                                                     unsigned long long* __restrict__ keys,
+                                                     u32* __restrict__ vals, u32* __restrict__ qOf,
+                                                     u32* __restrict__ dcol, u32* __restrict__ dout) {
+    __shared__ u32 wsum[4];
+    const u32 off = doff[blockIdx.x];
+    if (off == NULLV) return;  // kept tile (uniform)
+    const u32 t = t0 + blockIdx.x;
+    const u32 slot = threadIdx.x, w = slot >> 6, l = slot & 63;
+    const u32 idx = blockValues[static_cast<size_t>(t) * TILE + slot];
+    const bool v = idx != NULLV;
+    const u64 m = __ballot(v);
+    if (l == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    if (!v) return;
+    u32 r = __popcll(m & ((1ull << l) - 1));
+    for (u32 k = 0; k < w; ++k) r += wsum[k];
+    const u32 j = off + r;  // among the demoted entries
+    const u32 q = tilePanel[t].x * 16 + slot / 16 - qa;
+    const u32 c = denseCols[static_cast<size_t>(t) * 16 + slot % 16];
+    keys[n0 + j] = static_cast<unsigned long long>(q / RB) * N + c;
+    vals[n0 + j] = n0 + j;
+    qOf[n0 + j] = q;
+    dcol[j] = c;
+    dout[j] = idx;
+}
+
+// local entry e < n0: residual entry e (arrays offset to the range); else demoted entry e - n0
 __global__ void k_rb_gather(const u32* __restrict__ order, const u32* __restrict__ qOf,
                             const u32* __restrict__ sparseColIdx,
-                            const u32* __restrict__ sparseValues, u32 n, u32 RB,
+                            const u32* __restrict__ sparseValues, const u32* __restrict__ dcol,
+                            const u32* __restrict__ dout, u32 n0, u32 n, u32 RB,
                             u32* __restrict__ meta, u32* __restrict__ out, u32* __restrict__ rbEnd) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const u32 e = order[i];
     const u32 q = qOf[e];
-    meta[i] = ((q % RB) << 22) | sparseColIdx[e];
-    out[i] = sparseValues[e];
+    meta[i] = ((q % RB) << 22) | (e < n0 ? sparseColIdx[e] : dcol[e - n0]);
+    out[i] = e < n0 ? sparseValues[e] : dout[e - n0];
     const u32 rb = q / RB;
     if (i + 1 == n || qOf[order[i + 1]] / RB != rb) rbEnd[rb] = i + 1;
 }
@@ -842,18 +889,21 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
 }
 }  // namespace
 
-const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, u32 pa, u32 pb, int* err) const {
+const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, bool half, u32 pa, u32 pb,
+                                                  int* err) const {
     *err = BSMR_OK;
+    const u32 tmin = half ? tile_min_half : tile_min_f32;
     if (pa == 0 && pb == P) {
-        const int slot = rowBytes == 256 ? 0 : rowBytes == 512 ? 1 : rowBytes == 1024 ? 2 : 3;
+        const int slot = (rowBytes == 256 ? 0 : rowBytes == 512 ? 1 : rowBytes == 1024 ? 2 : 3) + (half ? 4 : 0);
         RowBlockLayout& L = rbl[slot];
-        if (L.rowBytes != rowBytes) *err = build_rowblock_layout(L, rowBytes, 0, P);
+        if (L.rowBytes != rowBytes || L.tileMin != tmin)
+            *err = build_rowblock_layout(L, rowBytes, 0, P, tmin);
         return *err == BSMR_OK ? &L : nullptr;
     }
     for (const auto& L : shard_rbl)
-        if (L->rowBytes == rowBytes && L->pa == pa && L->pb == pb) return L.get();
+        if (L->rowBytes == rowBytes && L->pa == pa && L->pb == pb && L->tileMin == tmin) return L.get();
     auto L = std::make_unique<RowBlockLayout>();
-    *err = build_rowblock_layout(*L, rowBytes, pa, pb);
+    *err = build_rowblock_layout(*L, rowBytes, pa, pb, tmin);
     if (*err != BSMR_OK) return nullptr;
     if (shard_rbl.size() >= MAX_SHARD_LAYOUTS) shard_rbl.erase(shard_rbl.begin());
     shard_rbl.push_back(std::move(L));
@@ -861,7 +911,7 @@ const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, u32 pa, u32 pb, 
 }
 
 // Row-block launch layout over panels [pa, pb) (the whole plan, or one row-panel shard).
-int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb) const {
+int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin) const {
     L.rowBytes = 0;
     hipStream_t s = stream;
     if (N > (1u << 22)) {
@@ -880,28 +930,66 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb)
         cus = 256;
     const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
     const u32 ebase = h_sparseValueOffsets[pa];
-    const u32 n = h_sparseValueOffsets[pb] - ebase;
+    const u32 n0 = h_sparseValueOffsets[pb] - ebase;  // residual entries of the range
+    // dense tiles of the range: kept (>= tileMin stored entries) or demoted to entries
+    const u32 T0 = h_blockOffsets[pa], nT = h_blockOffsets[pb] - T0;
+    std::vector<u32> tcnt(nT, 0), doff(nT, NULLV), keptPos(nT + 1ull, 0), hkept;
+    u32 nd = 0;
+    if (nT && tileMin > 0) {
+        DevBuf<u32> dcnt;
+        BSMR_CHECK(dcnt.alloc(nT));
+        hipLaunchKernelGGL(k_tile_nnz, dim3(nT), dim3(256), 0, s, blockValues.data(), T0, dcnt.data());
+        BSMR_HIP(hipGetLastError());
+        BSMR_HIP(hipMemcpyAsync(tcnt.data(), dcnt.data(), nT * sizeof(u32), hipMemcpyDeviceToHost, s));
+        BSMR_HIP(hipStreamSynchronize(s));
+    }
+    for (u32 t = 0; t < nT; ++t) {
+        keptPos[t] = static_cast<u32>(hkept.size());
+        if (tileMin > 0 && tcnt[t] < tileMin) {
+            doff[t] = nd;
+            nd += tcnt[t];
+        } else {
+            hkept.push_back(T0 + t);
+        }
+    }
+    keptPos[nT] = static_cast<u32>(hkept.size());
+    const u32 n = n0 + nd;
+    if (hkept.empty())
+        BSMR_CHECK(L.tileIds.alloc(1));
+    else
+        BSMR_CHECK(L.tileIds.upload(hkept.data(), hkept.size(), s));
     BSMR_CHECK(L.meta.alloc(std::max<u32>(n, 1)));
     BSMR_CHECK(L.out.alloc(std::max<u32>(n, 1)));
     std::vector<u32> rbEnd(nRB, 0), hmeta(n);
     if (n) {
         DevBuf<unsigned long long> keys, skeys;
-        DevBuf<u32> vals, order, qOf, dEnd;
+        DevBuf<u32> vals, order, qOf, dEnd, ddoff, dcol, dout;
         BSMR_CHECK(keys.alloc(n));
         BSMR_CHECK(skeys.alloc(n));
         BSMR_CHECK(vals.alloc(n));
         BSMR_CHECK(order.alloc(n));
         BSMR_CHECK(qOf.alloc(n));
         BSMR_CHECK(dEnd.alloc(nRB));
+        BSMR_CHECK(dcol.alloc(std::max<u32>(nd, 1)));
+        BSMR_CHECK(dout.alloc(std::max<u32>(nd, 1)));
         BSMR_HIP(hipMemsetAsync(dEnd.data(), 0, nRB * sizeof(u32), s));
-        hipLaunchKernelGGL(k_rb_keys, dim3(pb - pa), dim3(256), 0, s, sparseValueOffsets.data(),
-                           sparseRel.data(), sparseColIdx.data(), pa, RBr, N, keys.data(),
-                           vals.data(), qOf.data());
+        if (pb > pa)
+            hipLaunchKernelGGL(k_rb_keys, dim3(pb - pa), dim3(256), 0, s, sparseValueOffsets.data(),
+                               sparseRel.data(), sparseColIdx.data(), pa, RBr, N, keys.data(),
+                               vals.data(), qOf.data());
+        if (nd) {
+            BSMR_CHECK(ddoff.upload(doff.data(), nT, s));
+            hipLaunchKernelGGL(k_tile_demote, dim3(nT), dim3(256), 0, s, blockValues.data(),
+                               denseItems.data(), denseCols.data(), T0, ddoff.data(), qa, RBr, N, n0,
+                               keys.data(), vals.data(), qOf.data(), dcol.data(), dout.data());
+        }
+        BSMR_HIP(hipGetLastError());
         BSMR_CHECK(sort_pairs64(keys.data(), skeys.data(), vals.data(), order.data(), n,
                                 bits_for(static_cast<u64>(nRB) * N), tmp, s));
         hipLaunchKernelGGL(k_rb_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
-                           qOf.data(), sparseColIdx.data() + ebase, sparseValues.data() + ebase, n, RBr,
-                           L.meta.data(), L.out.data(), dEnd.data());
+                           qOf.data(), sparseColIdx.data() + ebase, sparseValues.data() + ebase,
+                           dcol.data(), dout.data(), n0, n, RBr, L.meta.data(), L.out.data(),
+                           dEnd.data());
         BSMR_HIP(hipGetLastError());
         BSMR_HIP(hipMemcpyAsync(rbEnd.data(), dEnd.data(), nRB * sizeof(u32), hipMemcpyDeviceToHost, s));
         BSMR_HIP(hipMemcpyAsync(hmeta.data(), L.meta.data(), n * sizeof(u32), hipMemcpyDeviceToHost, s));
@@ -939,7 +1027,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb)
     for (u32 b = 0; b < nRB; ++b) {
         const u32 eb0 = b ? rbEnd[b - 1] : 0, eb1 = rbEnd[b];
         const u32 p0 = std::min(pa + b * (RBr / 16), pb), p1 = std::min(pa + (b + 1) * (RBr / 16), pb);
-        const u32 t0 = h_blockOffsets[p0], nt = h_blockOffsets[p1] - t0;
+        // kept tiles of the row block: positions [t0, t0 + nt) of the kept list
+        const u32 t0 = keptPos[h_blockOffsets[p0] - T0], nt = keptPos[h_blockOffsets[p1] - T0] - t0;
         u32 lo = eb0;
         for (u32 k = 0; k < NCR; ++k) {
             const size_t i = static_cast<size_t>(b) * NCR + k;
@@ -1087,6 +1176,14 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb)
         pieces.insert(pieces.end(), mine.begin(), mine.end());
         ends[i] = static_cast<u32>(pieces.size());
     }
+    L.rbCost.assign(nRB, 0.0);
+    for (size_t i = 0; i < items.size(); ++i) {
+        const uint4 it = items[i];
+        if (it.y == it.z && it.w == ends[i]) continue;  // padding
+        u64 ent = 0;
+        for (u32 k = it.w; k < ends[i]; ++k) ent += (pieces[k].y >> 22) + 1;
+        L.rbCost[it.x] += static_cast<double>(ent) + (ends[i] - it.w) + 16.0 * (it.z - it.y) + RBr;
+    }
     L.nItems = static_cast<u32>(items.size());
     L.nPieces = static_cast<u32>(pieces.size());
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
@@ -1100,6 +1197,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb)
     L.pa = pa;
     L.pb = pb;
     L.rowEnd = qend;
+    L.tileMin = tileMin;
+    L.nTilesKept = static_cast<u32>(hkept.size());
+    L.nDemoted = nd;
     L.rowBytes = rowBytes;
     return BSMR_OK;
 }

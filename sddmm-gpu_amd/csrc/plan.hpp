@@ -89,21 +89,37 @@ struct Plan {
         // panels [pa, pb) covered (the whole plan: 0, P); row block b starts at reordered
         // position 16 * pa + b * RB; rows at or past rowEnd = min(R, 16 * pb) are not staged
         u32 pa = 0, pb = 0, rowEnd = 0;
+        // dense tiles run as MFMA tiles only with >= tileMin stored entries; the entries of the
+        // others join the residual entries (fp32 MFMA has no rate advantage over vector FMA, so a
+        // sparse fp32 tile costs more than its entries' dot products)
+        u32 tileMin = 0, nTilesKept = 0, nDemoted = 0;
+        DevBuf<u32> tileIds;  // kept tile ids; item tile ranges index this list
         size_t lds = 0;
         DevBuf<u32> meta;   // local row << 22 | column
         DevBuf<u32> out;    // output index (CSR position)
         DevBuf<uint4> items;
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}
+        // per row block: Σ over its items of (entries + pieces + 16 tiles + RB staged rows), the
+        // shard cost model of bsmr_plan_shard
+        std::vector<double> rbCost;
     };
-    static constexpr int N_RB_LAYOUTS = 4;  // rows of 256, 512, 1024 and 2048 bytes
+    // rows of 256, 512, 1024 and 2048 bytes, for fp32 [0, 4) and fp16/bf16 [4, 8) (tileMin)
+    static constexpr int N_RB_LAYOUTS = 8;
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
+    // stored entries a dense tile needs to run on MFMA in the row-block launch (BSMR_TILE_MIN_F32
+    // / BSMR_TILE_MIN_HALF); 0 = every tile. Measured (r01k sweep, profiles/r01k/tile_min.json):
+    // fp32 MFMA (16x16x4) runs at the vector-FMA rate on gfx950 and a tile pays its empty slots,
+    // so every fp32 tile is cheaper as residual entries (257: none kept; C2 14.4 -> 12.9 us);
+    // fp16/bf16 MFMA is 8x the v_dot2 rate, so half tiles stay unless under half full
+    u32 tile_min_f32 = 257, tile_min_half = 128;
     // layouts of panel ranges (row-panel shards, bsmr_sddmm_panels), most recent last
     static constexpr size_t MAX_SHARD_LAYOUTS = 16;
     mutable std::vector<std::unique_ptr<RowBlockLayout>> shard_rbl;
-    int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb) const;
-    // the (cached) layout for rows of rowBytes over panels [pa, pb); null on error
-    const RowBlockLayout* rowblock_layout(u32 rowBytes, u32 pa, u32 pb, int* err) const;
+    int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin) const;
+    // the (cached) layout for rows of rowBytes over panels [pa, pb) for fp32 (half = false) or
+    // fp16/bf16 operands; null on error
+    const RowBlockLayout* rowblock_layout(u32 rowBytes, bool half, u32 pa, u32 pb, int* err) const;
 
     mutable DevBuf<uint8_t> tmp;  // scan/sort scratch
     // BSMR_DIAG & 32 debug timeline (4 u64 per wave of the last launch)
@@ -123,6 +139,9 @@ struct Plan {
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
+
+// the whole plan's row-block layout for (K, dtype) (sddmm.hip); *out = null for column-major
+int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out);
 
 }  // namespace bsmr
 

@@ -405,6 +405,7 @@ struct RbArgs {
     const u32* meta;        // local row << 22 | column
     const u32* out;
     const uint4* tilePanel;  // dense work items: .x = panel of the tile
+    const u32* tileIds;      // the layout's kept tiles: item tile ranges index this list
     const u32* denseCols;
     const u32* blockValues;
     u32 mode;  // 1 = dense tiles, 2 = residual, 3 = both
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     DenseTileLds<DT, RBY> dt;
     // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
     const u32 tw = NW - 1 - w;
-    if (tw < ntile) dt.load(a, it.y + tw, q0, tb);
+    if (tw < ntile) dt.load(a, a.tileIds[it.y + tw], q0, tb);
     Piece<RBY> pc;
     pc.len = 0;
     if (gr < np) load_piece<RBY>(a, it.w + gr, sub, rot, pre, pc);
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     }
     for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
-        dt.load(a, t, q0, tb);
+        dt.load(a, a.tileIds[t], q0, tb);
         dt.run(a, As, tb);
     }
     trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
@@ -816,10 +817,11 @@ int rb_slot(const Plan& p, u32 K, int dtype) {
 }
 
 // the row-block layout of panels [pa, pb) for slot's row size (built on first use)
-int get_rb_layout(const Plan& p, int slot, u32 pa, u32 pb, const Plan::RowBlockLayout** out) {
+int get_rb_layout(const Plan& p, int slot, int dtype, u32 pa, u32 pb,
+                  const Plan::RowBlockLayout** out) {
     std::lock_guard<std::mutex> g(p.layout_mu);
     int err = BSMR_OK;
-    *out = p.rowblock_layout(256u << slot, pa, pb, &err);
+    *out = p.rowblock_layout(256u << slot, dtype != BSMR_F32, pa, pb, &err);
     return err;
 }
 
@@ -842,6 +844,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.meta = L.meta.data();
     a.out = L.out.data();
     a.tilePanel = p.denseItems.data();
+    a.tileIds = L.tileIds.data();
     a.denseCols = p.denseCols.data();
     a.blockValues = p.blockValues.data();
     a.mode = mode;
@@ -897,6 +900,16 @@ int launch_panels(SddmmArgs a, hipStream_t s) {
 }
 
 }  // namespace
+
+// the whole plan's row-block layout for (K, dtype), built on first use; *out = null when that
+// (K, dtype) runs the column-major launch
+int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out) {
+    *out = nullptr;
+    const int slot = rb_slot(p, K, dtype);
+    if (slot < 0) return BSMR_OK;
+    return get_rb_layout(p, slot, dtype, 0, p.P, out);
+}
+
 }  // namespace bsmr
 
 using namespace bsmr;
@@ -925,7 +938,7 @@ extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const
         const int slot = rb_slot(p, K, dtype);
         if (slot >= 0) {
             const Plan::RowBlockLayout* L = nullptr;
-            BSMR_CHECK(get_rb_layout(p, slot, 0, p.P, &L));
+            BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
             BSMR_CHECK(launch_rb(p, *L, A, B, P, dtype, 3, s, nb));
             continue;
         }
@@ -964,7 +977,7 @@ extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const vo
     const int slot = rb_slot(p, K, dtype);
     if (slot >= 0) {
         const Plan::RowBlockLayout* L = nullptr;
-        BSMR_CHECK(get_rb_layout(p, slot, p0, p1, &L));
+        BSMR_CHECK(get_rb_layout(p, slot, dtype, p0, p1, &L));
         return launch_rb(p, *L, dA, dB, dP, dtype, 3, static_cast<hipStream_t>(stream));
     }
     if (dtype != BSMR_F32) {
@@ -1009,7 +1022,7 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     for (auto& e : ev) BSMR_HIP(hipEventCreate(&e));
     const int slot = rb_slot(p, K, dtype);
     const Plan::RowBlockLayout* L = nullptr;
-    if (slot >= 0) BSMR_CHECK(get_rb_layout(p, slot, 0, p.P, &L));
+    if (slot >= 0) BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
     SddmmArgs full = make_args(p, dA, dB, K, dP);
     full.nd = p.nDenseItems;
     full.nslots = p.nSlots;

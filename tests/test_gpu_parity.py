@@ -194,7 +194,7 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     and the column-major fallback (fp32 K=32): every output written once, by its own shard."""
     M, N, rp, ci = small_cases()["zipf"]
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
-    shards = [plan.shard(K, r, world) for r in range(world)]
+    shards = [plan.shard(K, r, world, dtype) for r in range(world)]
     A = make_data(M * K)
     B = make_data(N * K)
     P = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
