@@ -158,9 +158,9 @@ def chung_lu(n, nnz_target, seed, exponent=2.2, chunk=20_000_000):
         keys.append(j.astype(np.int64) * n + i)
         drawn += m
     key = np.unique(np.concatenate(keys))
-    rows = key // n
+    del keys
     rowptr = np.zeros(n + 1, dtype=np.int64)
-    np.add.at(rowptr, rows + 1, 1)
+    rowptr[1:] = np.bincount(key // n, minlength=n)
     return n, n, np.cumsum(rowptr).astype(np.uint32), (key % n).astype(np.uint32)
 
 

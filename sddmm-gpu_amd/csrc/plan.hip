@@ -159,6 +159,8 @@ struct ClusterArgs {
     u32* state;
     u32* st;
     u32* ctrl;          // [0] abort, [1] timeout, [2..3] exact evals (u64), [4..5] total evals
+    u32* cmpScratch;    // [gridDim.x][nbpr] zeros: dense row image of the exact path (global,
+                        // so a cluster's LDS is its representative only: more resident clusters)
     u32 M, nbpr, B, keptMask, c0;
     float alpha;
     int exact_all;
@@ -212,9 +214,9 @@ __device__ float sim_exact(const u32* rep, const u32* cmp, u32 nbpr, u32 B, u32 
 
 __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
     extern __shared__ __attribute__((aligned(16))) u32 smem[];
-    u32* rep = smem;                               // nbpr
-    u32* cmp = smem + ((a.nbpr + 3) & ~3u);        // nbpr (exact path only)
-    float* smn = reinterpret_cast<float*>(cmp + ((a.nbpr + 3) & ~3u));  // 32
+    u32* rep = smem;                                                    // nbpr
+    float* smn = reinterpret_cast<float*>(smem + ((a.nbpr + 3) & ~3u));  // 32
+    u32* cmp = a.cmpScratch + static_cast<size_t>(blockIdx.x) * a.nbpr;  // zero between uses
     float* smx = smn + 32;
     __shared__ u32 s_abort;
     const u32 l = lane_id();
@@ -296,10 +298,7 @@ __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
         st_agent(&a.st[k], start + 2);
     }
     // representative = encoding of the start row
-    for (u32 x = l; x < a.nbpr; x += 64) {
-        rep[x] = 0;
-        cmp[x] = 0;
-    }
+    for (u32 x = l; x < a.nbpr; x += 64) rep[x] = 0;
     __syncthreads();
     u32 SR, SC0;
     u64 S1R;
@@ -333,15 +332,38 @@ __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        u64 todo = __ballot(!(v & ASSIGNED) && l < L);
+        const bool mine = !(v & ASSIGNED) && l < L;
+        u64 todo = __ballot(mine);
+        // the batch's row metadata in one round trip (lane j: position i + j), and each
+        // position's first 64 encoding entries loaded while the previous position computes; the
+        // representative (LDS) is the only state an accept changes, so the loads are order-free
+        u32 m_b0 = 0, m_nb = 0, m_sc = 0, m_s1 = 0;
+        if (mine) {
+            const u32 row = a.asc[idx];
+            m_b0 = a.rowptr[row];
+            m_nb = a.nblk[row];
+            m_sc = a.SC[row];
+            m_s1 = a.S1C[row];
+        }
+        u32 ent0 = 0;
+        if (todo) {
+            const u32 jn = __builtin_ctzll(todo);
+            const u32 nb0 = __shfl(m_b0, jn), nnb = __shfl(m_nb, jn);
+            ent0 = l < nnb ? a.enc[nb0 + l] : 0u;
+        }
         while (todo) {
             const u32 j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const u32 pos = i + j;
-            const u32 row = a.asc[pos];
-            const u32 b0 = a.rowptr[row], nb = a.nblk[row];
-            const u32 SCr = a.SC[row];
-            const u32 S1Cr = a.S1C[row];
+            const u32 b0 = __shfl(m_b0, j), nb = __shfl(m_nb, j);
+            const u32 SCr = __shfl(m_sc, j);
+            const u32 S1Cr = __shfl(m_s1, j);
+            const u32 cur0 = ent0;  // enc[b0 + l] (l < nb)
+            if (todo) {
+                const u32 jn = __builtin_ctzll(todo);
+                const u32 nb0 = __shfl(m_b0, jn), nnb = __shfl(m_nb, jn);
+                ent0 = l < nnb ? a.enc[nb0 + l] : 0u;
+            }
             ++ntotal;
             bool accept;
             if (SR == 0 && SCr == 0) {
@@ -356,7 +378,7 @@ __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
                 if (!a.exact_all) {
                     double mn = 0.0;
                     for (u32 e = l; e < nb; e += 64) {
-                        const u32 ent = a.enc[b0 + e];
+                        const u32 ent = e < 64 ? cur0 : a.enc[b0 + e];
                         const u32 blk = ent & 0xFFFFu;
                         const u32 rv = rep[blk];
                         if (rv && kept_idx(blk, a.B, a.keptMask))
@@ -389,7 +411,7 @@ __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
             if (accept) {
                 u32 dsr = 0, ds1 = 0;
                 for (u32 e = l; e < nb; e += 64) {
-                    const u32 ent = a.enc[b0 + e];
+                    const u32 ent = e < 64 ? cur0 : a.enc[b0 + e];
                     const u32 blk = ent & 0xFFFFu, c = ent >> 16;
                     const u32 o = rep[blk], nv = o + c;
                     rep[blk] = nv;
@@ -1266,11 +1288,20 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     ca.alpha = alpha;
     ca.exact_all = exact_all;
     ca.timeout_ticks = 100ull * 1000 * 1000 * 20;  // 20 s without progress
-    const size_t lds_cl = (2 * ((nbpr + 3) & ~3u) + 64) * sizeof(u32);
+    const size_t lds_cl = (((nbpr + 3) & ~3u) + 64) * sizeof(u32);
+    // clusters per launch: a launch's clusters are dispatched in order and each waits only for
+    // its predecessor, so more clusters than fit on the chip at once cannot deadlock (later ones
+    // start as earlier ones finish); capped by the exact path's scratch (<= 256 MiB)
+    const u32 Rmax = static_cast<u32>(std::max<u64>(
+        64, std::min<u64>(cluster_batch, (64ull << 20) / std::max<u32>(nbpr, 1))));
+    DevBuf<u32> cmpScratch;
+    BSMR_CHECK(cmpScratch.alloc(static_cast<size_t>(Rmax) * nbpr));
+    BSMR_HIP(hipMemsetAsync(cmpScratch.data(), 0, static_cast<size_t>(Rmax) * nbpr * sizeof(u32), s));
+    ca.cmpScratch = cmpScratch.data();
     u32 c0 = 1;
     u32 last_valid = 0;
     while (c0 <= M) {  // at most M - z clusters
-        const u32 R = std::min<u32>(cluster_batch, M + 1 - c0);
+        const u32 R = std::min<u32>(Rmax, M + 1 - c0);
         ca.c0 = c0;
         hipLaunchKernelGGL(k_cluster, dim3(R), dim3(64), lds_cl, s, ca);
         BSMR_HIP(hipGetLastError());

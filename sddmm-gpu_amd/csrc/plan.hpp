@@ -43,7 +43,9 @@ struct Plan {
     u32 piece_order = 0;
     // L2 budget of one column range of the row-block layout (KiB; BSMR_L2_RANGE_KB)
     u32 l2_range_kb = 2048;
-    u32 cluster_batch = 512;
+    // clusters per persistent clustering launch (bsmr_plan_options.cluster_batch); r01k timing
+    // on reddit_like x0.25: 512 -> 9.7 s, 4096 -> 4.6 s, 16384 -> 2.3 s (fewer host round trips, more in flight)
+    u32 cluster_batch = 16384;
 
     // input
     DevBuf<u32> rowptr, colidx;

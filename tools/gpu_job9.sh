@@ -1,0 +1,8 @@
+set -o pipefail
+O=gpurun_out/j9
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu -k "plan or golden or exact or smoke or cluster" --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 &&
+timeout -k 10 300 python3 tools/plan_time.py --workload nips_like --batches 512,2048 > $O/plan_c2.json 2> $O/err.log &&
+timeout -k 10 400 python3 tools/plan_time.py --workload reddit_like --scale 0.25 --batches 4096,8192,16384 > $O/plan_c4q.json 2>> $O/err.log &&
+timeout -k 10 600 python3 tools/plan_time.py --workload reddit_like --scale 0.5 --batches 8192 > $O/plan_c4h.json 2>> $O/err.log
