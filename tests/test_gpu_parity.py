@@ -213,6 +213,40 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
         assert O.check_data(ref[mine], part[mine]) == 0
 
 
+@pytest.mark.parametrize("env,K,dtype", [
+    ({"BSMR_TILE_MIN_F32": "0"}, 128, 0),      # every fp32 tile on MFMA
+    ({"BSMR_TILE_MIN_F32": "100"}, 128, 0),    # some tiles demoted to residual entries
+    ({"BSMR_TILE_MIN_F32": "257"}, 64, 0),     # none kept (default)
+    ({"BSMR_TILE_MIN_HALF": "0"}, 256, 1),
+    ({"BSMR_TILE_MIN_HALF": "200"}, 256, 2),
+    ({"BSMR_TILE_MIN_HALF": "257"}, 512, 2),
+    ({"BSMR_L2_RANGE_KB": "64"}, 128, 0),      # m > 1 column ranges per XCD, several rounds
+    ({"BSMR_L2_RANGE_KB": "64", "BSMR_TILE_MIN_F32": "0"}, 64, 0),
+    ({"BSMR_L2_RANGE_KB": "64"}, 256, 1),
+    ({"BSMR_PIECE_ORDER": "1"}, 128, 0),
+])
+def test_rowblock_layout_variants(monkeypatch, env, K, dtype):
+    """Launch-layout switches (tile demotion thresholds, L2 column ranges, piece order) on the
+    blocky pattern (dense tiles and residual entries) and a zipf pattern: values unchanged."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for name in ("blocky", "wide_bs20"):
+        M, N, rp, ci = small_cases()[name]
+        plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock")
+        A = make_data(M * K)
+        B = make_data(N * K)
+        P = run_sddmm(plan, A, B, K, len(ci), dtype=dtype)
+        if dtype:
+            A, B = half_values(A, dtype), half_values(B, dtype)
+        ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
+        assert np.isfinite(P).all(), name
+        assert O.check_data(ref, P) == 0, name
+        # shards of the same plan agree
+        shards = [plan.shard(K, r, 3, dtype) for r in range(3)]
+        Ps = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
+        assert np.isfinite(Ps).all() and O.check_data(ref, Ps) == 0, name
+
+
 def test_values_independent_of_layout_permutation():
     """Size-independent property: P of the same S is identical for every alpha/delta plan."""
     M, N, rp, ci = small_cases()["zipf"]
