@@ -942,17 +942,32 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     }
     const u32 qa = 16 * pa, qend = std::min(R, 16 * pb);
     const u32 Rs = qend > qa ? qend - qa : 0;  // reordered rows of the range
-    const u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, Rs);
-    const u32 nRB = std::max<u32>(1, (Rs + RBr - 1) / RBr);
-    const size_t lds = static_cast<size_t>(RBr) * rowBytes;
-    const u32 NT = lds > 80 * 1024 ? 1024 : 512;
-    const u32 wgPerCU = std::max<u32>(1, std::min<u32>(static_cast<u32>(160 * 1024 / lds), 2048 / NT));
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
     const u32 ebase = h_sparseValueOffsets[pa];
     const u32 n0 = h_sparseValueOffsets[pb] - ebase;  // residual entries of the range
+    u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, Rs);
+    {
+        // sparse rows (< 64 stored entries per row: banded / FEM patterns) keep their row blocks
+        // whole, one item each; when there are more row blocks than workgroup slots, use the
+        // smallest row block that needs no more rounds of slots, so the last round is full
+        // (cop20k-like C3: 421 blocks of 288 rows = 1.6 rounds -> 505 blocks of 240 rows)
+        const size_t lds0 = static_cast<size_t>(RBr) * rowBytes;
+        const u32 slots = static_cast<u32>(cus) * (lds0 > 80 * 1024 ? 1u : 2u);
+        const u32 nRB0 = (Rs + RBr - 1) / std::max<u32>(RBr, 1);
+        if (Rs && n0 < 64ull * Rs && nRB0 > slots) {
+            const u32 rounds = (nRB0 + slots - 1) / slots;
+            const u32 rb = (Rs + rounds * slots - 1) / (rounds * slots);
+            RBr = std::min(RBr, std::max<u32>(16, (rb + 15) / 16 * 16));
+        }
+    }
+    const u32 nRB = std::max<u32>(1, (Rs + RBr - 1) / RBr);
+    const size_t lds = static_cast<size_t>(RBr) * rowBytes;
+    const u32 NT = lds > 80 * 1024 ? 1024 : 512;
+    // k_sddmm_rb takes 160 KiB (1024 threads) or 80 KiB (512) of LDS per workgroup
+    const u32 wgPerCU = NT == 1024 ? 1 : 2;
+    const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
     // dense tiles of the range: kept (>= tileMin stored entries) or demoted to entries
     const u32 T0 = h_blockOffsets[pa], nT = h_blockOffsets[pb] - T0;
     std::vector<u32> tcnt(nT, 0), doff(nT, NULLV), keptPos(nT + 1ull, 0), hkept;
