@@ -306,8 +306,12 @@ def main():
     rby = K * (4 if dtype == F32 else 2)
     tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
     if rby in (256, 512, 1024, 2048) and args.layout != "colmajor" and not tile_dominated:
-        kern = (f"k_sddmm_rb<{dtype},{rby},1024> (row-block LDS layout, {rby}-byte rows: "
-                "dense-tile MFMA + residual)")
+        tiles = ("fp32 tiles demoted to residual entries" if dtype == F32
+                 else "dense-tile MFMA for tiles >= 128 entries")
+        rows = st_after["rb_rows"][{256: 0, 512: 1, 1024: 2, 2048: 3}[rby]]
+        nt = 1024 if rby * rows > 80 * 1024 else 512
+        kern = (f"k_sddmm_rb<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
+                f"rows per block: residual entries; {tiles})")
     elif dtype == F32:
         kern = f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)"
     else:
