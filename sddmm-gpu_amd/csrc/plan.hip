@@ -1077,10 +1077,10 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                                : eb1;
             se0[i] = lo;
             se1[i] = hi;
-            for (u32 e = lo; e < hi;) {  // column runs cut every RB_PIECE_MAX entries
+            for (u32 e = lo; e < hi;) {  // column runs cut every piece_max entries
                 const u32 col = hmeta[e] & CM;
                 u32 f = e + 1;
-                while (f < hi && f - e < RB_PIECE_MAX && (hmeta[f] & CM) == col) ++f;
+                while (f < hi && f - e < piece_max && (hmeta[f] & CM) == col) ++f;
                 ++spc[i];
                 e = f;
             }
@@ -1186,7 +1186,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             ends[j * XCD_BUCKETS + x] = lends[x][j];
         }
     // column-run pieces: each item's entries [e0, e1) cut at column changes and every
-    // RB_PIECE_MAX entries; piece {first entry, column | (length - 1) << 22}. A workgroup's NG
+    // piece_max (<= RB_PIECE_MAX) entries; piece {first entry, column | (length - 1) << 22}. A workgroup's NG
     // row-groups take one piece each per phase, so phase ph runs the item's pieces
     // [ph NG, (ph + 1) NG). Longest first, so the 16 row-groups of a wave get pieces of similar
     // length: over the whole item (piece_order 0), or inside column windows of one phase
@@ -1202,7 +1202,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         for (u32 e = ea; e < eb;) {
             const u32 col = hmeta[e] & CM;
             u32 f = e + 1;
-            while (f < eb && f - e < RB_PIECE_MAX && (hmeta[f] & CM) == col) ++f;
+            while (f < eb && f - e < piece_max && (hmeta[f] & CM) == col) ++f;
             mine.push_back(make_uint2(e, col | ((f - e - 1) << 22)));
             e = f;
         }

@@ -43,6 +43,8 @@ struct Plan {
     u32 piece_order = 0;
     // L2 budget of one column range of the row-block layout (KiB; BSMR_L2_RANGE_KB)
     u32 l2_range_kb = 2048;
+    // entries per column-run piece of the row-block layout (<= RB_PIECE_MAX; BSMR_PIECE_MAX)
+    u32 piece_max = RB_PIECE_MAX;
     // clusters per persistent clustering launch (bsmr_plan_options.cluster_batch); r01k timing
     // on reddit_like x0.25: 512 -> 9.7 s, 4096 -> 4.6 s, 16384 -> 2.3 s (fewer host round trips, more in flight)
     u32 cluster_batch = 16384;
