@@ -205,8 +205,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local)
-        D.init("nccl")  # RCCL over xGMI
+        # one rank per GPU; BSMR_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
+        # multi-process path (ranks then share devices; their timings are not a measurement)
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        D.init(os.environ.get("BSMR_DIST_BACKEND", "nccl"))  # nccl = RCCL over xGMI
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
