@@ -128,6 +128,28 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
     }
 
 
+def rowblock_bounds(st, rby, ms):
+    """The row-block kernel's on-chip traffic per launch against the rates that bound it
+    (MI355X_MICROARCH.md, measured): L2 -> CU ingest (A row blocks staged once per item, one B row
+    per column-run piece, 8 B of metadata per entry and per piece, a B tile per MFMA tile) at
+    16.8-18.8 TB/s chip-wide for gathered rows served from L2, and LDS reads (one A row per
+    residual entry, 16 A rows per tile) at ~150 TB/s (ds_read_b128, every CU streaming)."""
+    i = {256: 0, 512: 1, 1024: 2, 2048: 3}[rby]
+    rows, items, pieces = st["rb_rows"][i], st["rb_work_items"][i], st["rb_pieces"][i]
+    entries, tiles = st["rb_entries"][i], st["rb_tiles"][i]
+    ingest = items * rows * rby + pieces * rby + 8.0 * (entries + pieces) + tiles * 16 * rby
+    lds = entries * rby + tiles * 16 * rby
+    t = ms * 1e-3
+    return {
+        "l2_to_cu": {"bytes": ingest, "achieved_TBps": round(ingest / t / 1e12, 2),
+                     "ref_TBps": 17.8, "frac": round(ingest / t / 17.8e12, 3)},
+        "lds_read": {"bytes": lds, "achieved_TBps": round(lds / t / 1e12, 2),
+                     "ref_TBps": 150.0, "frac": round(lds / t / 150e12, 3)},
+        "layout": {"rows_per_block": rows, "items": items, "pieces": pieces,
+                   "entries": entries, "mfma_tiles": tiles},
+    }
+
+
 def vendor_baseline(M, N, K, rp, ci, dA, dB, P_engine, dtype, stream, flops, engine_ms):
     """rocsparse_sddmm on the same device operands (the reference's cuSPARSE baseline,
     include/cuSparseSDDMM.cuh:27-145): preprocess once, then timed back-to-back calls, for the
@@ -354,6 +376,8 @@ def main():
         },
         "kernels_ms": {k: round(v, 5) for k, v in prof.items()},
     }
+    if kern.startswith("k_sddmm_rb"):
+        out["bounds"] = rowblock_bounds(st_after, rby, ms_per_step)
     if cold_ms is not None:
         out["cold"] = {"ms_per_step": round(cold_ms, 5),
                        "value": round(flops_rank * world / (cold_ms * 1e-3) / 1e9, 2),

@@ -58,7 +58,8 @@ class PlanStats(C.Structure):
                 ("row_reorder_ms", C.c_float), ("col_reorder_ms", C.c_float),
                 ("dense_items", C.c_uint32), ("residual_items", C.c_uint32),
                 ("rb_rows", C.c_uint32 * 4), ("rb_items", C.c_uint32 * 4),
-                ("rb_pieces", C.c_uint32 * 4)]
+                ("rb_pieces", C.c_uint32 * 4), ("rb_entries", C.c_uint32 * 4),
+                ("rb_tiles", C.c_uint32 * 4), ("rb_work_items", C.c_uint32 * 4)]
 
     def as_dict(self):
         d = {}
@@ -76,6 +77,8 @@ class EvalStats(C.Structure):
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
+
+ABI_VERSION = 2  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -110,6 +113,9 @@ def lib():
     vp = C.c_void_p
     L.bsmr_last_error.restype = C.c_char_p
     L.bsmr_abi_version.restype = C.c_int
+    if L.bsmr_abi_version() != ABI_VERSION:  # the structs below mirror include/bsmr.h
+        raise BsmrError(f"{LIB_PATH}: ABI {L.bsmr_abi_version()}, binding expects {ABI_VERSION} "
+                        "(rebuild with `make -C sddmm-gpu_amd`)")
     for f in ("bsmr_csr_load_mtx", "bsmr_csr_load_smtx", "bsmr_csr_load_snap", "bsmr_csr_load"):
         getattr(L, f).argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
     L.bsmr_csr_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p, C.POINTER(vp)]

@@ -135,6 +135,9 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_rows[i] = L.rowBytes ? L.RB : 0;
         s->rb_items[i] = L.rowBytes ? L.nItems : 0;
         s->rb_pieces[i] = L.rowBytes ? L.nPieces : 0;
+        s->rb_entries[i] = L.rowBytes ? L.nEntries : 0;
+        s->rb_tiles[i] = L.rowBytes ? L.nTilesKept : 0;
+        s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
     }
     return BSMR_OK;
 }

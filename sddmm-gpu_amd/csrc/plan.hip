@@ -1214,9 +1214,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         ends[i] = static_cast<u32>(pieces.size());
     }
     L.rbCost.assign(nRB, 0.0);
+    L.nWorkItems = 0;
     for (size_t i = 0; i < items.size(); ++i) {
         const uint4 it = items[i];
         if (it.y == it.z && it.w == ends[i]) continue;  // padding
+        ++L.nWorkItems;
         u64 ent = 0;
         for (u32 k = it.w; k < ends[i]; ++k) ent += (pieces[k].y >> 22) + 1;
         L.rbCost[it.x] += static_cast<double>(ent) + (ends[i] - it.w) + 16.0 * (it.z - it.y) + RBr;
@@ -1237,6 +1239,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     L.tileMin = tileMin;
     L.nTilesKept = static_cast<u32>(hkept.size());
     L.nDemoted = nd;
+    L.nEntries = n;
     L.rowBytes = rowBytes;
     return BSMR_OK;
 }

@@ -96,7 +96,7 @@ struct Plan {
         // dense tiles run as MFMA tiles only with >= tileMin stored entries; the entries of the
         // others join the residual entries (fp32 MFMA has no rate advantage over vector FMA, so a
         // sparse fp32 tile costs more than its entries' dot products)
-        u32 tileMin = 0, nTilesKept = 0, nDemoted = 0;
+        u32 tileMin = 0, nTilesKept = 0, nDemoted = 0, nEntries = 0, nWorkItems = 0;
         DevBuf<u32> tileIds;  // kept tile ids; item tile ranges index this list
         size_t lds = 0;
         DevBuf<u32> meta;   // local row << 22 | column
