@@ -420,7 +420,17 @@ typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ u32 lds_chunk(u32 lr, u32 c) { return (c & ~3u) | ((c & 3u) ^ (lr & 3u)); }
+// physical 16-byte chunk of logical chunk c of image row lr. fp16/bf16 images swizzle inside each
+// 64-byte quad so the MFMA tile reads (4 chunk-consecutive rows per lane group) spread over the
+// banks; fp32 images are plain (no tiles on the fp32 row-block path; the residual reads are
+// conflict-free by the rotation alone), which saves the swizzle arithmetic per entry.
+template <int DT>
+__device__ __forceinline__ u32 lds_chunk(u32 lr, u32 c) {
+    if constexpr (DT == 0)
+        return c;
+    else
+        return (c & ~3u) | ((c & 3u) ^ (lr & 3u));
+}
 
 __device__ __forceinline__ f32x4 ld16(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
 
@@ -538,7 +548,7 @@ struct DenseTileLds {
             if (k0) loadB(a, k0, bv);
 #pragma unroll
             for (int kk = 0; kk < CH; ++kk) {
-                const f32x4 av = ld16(arow + 16 * lds_chunk(lr, chunk(k0 + kk, g)));
+                const f32x4 av = ld16(arow + 16 * lds_chunk<DT>(lr, chunk(k0 + kk, g)));
                 f32x4& acc = (kk & 1) ? acc1 : acc0;
                 acc = chunk_mfma<DT>(av, bv[kk], acc);
             }
@@ -611,7 +621,7 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
                 default: m = group_bcast<G, G - 1>(pc.mm[k]); break;
             }
             const u32 lr = m >> 22;
-            const u32 ab = lr * RBY + 16 * (sub ^ (lr & 3));
+            const u32 ab = lr * RBY + 16 * lds_chunk<DT>(lr, sub);  // + rot[f]: chunk G t + sub
             f32x2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
             constexpr u32 H = NC > 4 ? NC / 2 : NC;  // LDS reads in flight per half
 #pragma unroll
@@ -689,22 +699,26 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         static_assert(MAXB * NW == (NT == 1024 ? 160u : 80u), "whole KiB blocks");
         static_assert(MAXB * NR <= 64, "one row index per lane");
         const u32 lane = tid & 63;
+        const u32 ws = __builtin_amdgcn_readfirstlane(w);  // wave index in an SGPR
         u32 rowv = 0;
         {
-            const u32 i = lane / NR, b = w + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
+            const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
             if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
         }
+        // the source chunk of lane l is the same in every block of the wave: x % NCH and
+        // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 16)
+        const u32 x0 = 64 * ws + lane;
+        const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
 #pragma unroll
         for (u32 i = 0; i < MAXB; ++i) {
-            const u32 b = w + i * NW;
-            const u32 x = 64 * b + lane, lr = x / NCH;
+            const u32 b = ws + i * NW;
             u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
 #pragma unroll
             for (u32 k = 1; k < NR; ++k) {
                 const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
                 src = lane / NCH == k ? rk : src;
             }
-            const char* g = a.A + static_cast<size_t>(src) * RBY + 16 * lds_chunk(lr, x % NCH);
+            const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                              (__attribute__((address_space(3))) void*)(As + 1024 * b),
                                              16, 0, 0);
