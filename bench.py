@@ -134,7 +134,7 @@ def rowblock_bounds(st, rby, ms):
     per column-run piece, 8 B of metadata per entry and per piece, a B tile per MFMA tile) at
     16.8-18.8 TB/s chip-wide for gathered rows served from L2, and LDS reads (one A row per
     residual entry, 16 A rows per tile) at ~150 TB/s (ds_read_b128, every CU streaming)."""
-    i = {256: 0, 512: 1, 1024: 2, 2048: 3}[rby]
+    i = {128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]
     rows, items, pieces = st["rb_rows"][i], st["rb_work_items"][i], st["rb_pieces"][i]
     entries, tiles = st["rb_entries"][i], st["rb_tiles"][i]
     ingest = items * rows * rby + pieces * rby + 8.0 * (entries + pieces) + tiles * 16 * rby
@@ -329,10 +329,10 @@ def main():
     # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
     rby = K * (4 if dtype == F32 else 2)
     tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
-    if rby in (256, 512, 1024, 2048) and args.layout != "colmajor" and not tile_dominated:
+    if rby in (128, 256, 512, 1024, 2048) and args.layout != "colmajor" and not tile_dominated:
         tiles = ("fp32 tiles demoted to residual entries" if dtype == F32
                  else "dense-tile MFMA for tiles >= 128 entries")
-        rows = st_after["rb_rows"][{256: 0, 512: 1, 1024: 2, 2048: 3}[rby]]
+        rows = st_after["rb_rows"][{128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]]
         nt = 1024 if rby * rows > 80 * 1024 else 512
         kern = (f"k_sddmm_rb<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
                 f"rows per block: residual entries; {tiles})")

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 2  /* 2: bsmr_plan_shard_dtype, rb_entries/rb_tiles/rb_work_items stats */
+#define BSMR_ABI_VERSION 3  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes) */
 
 typedef enum {
     BSMR_OK = 0,
@@ -121,12 +121,12 @@ typedef struct {
     float row_reorder_ms;            /* bsmr_rowReordering */
     float col_reorder_ms;            /* bsmr_colReordering (incl. tile layout) */
     uint32_t dense_items, residual_items;  /* work-list sizes of the SDDMM launch */
-    /* row-block layouts built so far (index 0..3: rows of 256/512/1024/2048 bytes; 0 = not
+    /* row-block layouts built so far (index 0..4: rows of 128/256/512/1024/2048 bytes; 0 = not
      * built): rows per block, workgroup items (incl. per-XCD padding), column-run pieces */
-    uint32_t rb_rows[4], rb_items[4], rb_pieces[4];
+    uint32_t rb_rows[5], rb_items[5], rb_pieces[5];
     /* the same layouts: residual entries (incl. entries of demoted tiles), MFMA tiles kept,
      * non-padding items */
-    uint32_t rb_entries[4], rb_tiles[4], rb_work_items[4];
+    uint32_t rb_entries[5], rb_tiles[5], rb_work_items[5];
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

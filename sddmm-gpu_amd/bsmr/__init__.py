@@ -57,9 +57,9 @@ class PlanStats(C.Structure):
                 ("exact_similarity_evals", C.c_uint64), ("total_similarity_evals", C.c_uint64),
                 ("row_reorder_ms", C.c_float), ("col_reorder_ms", C.c_float),
                 ("dense_items", C.c_uint32), ("residual_items", C.c_uint32),
-                ("rb_rows", C.c_uint32 * 4), ("rb_items", C.c_uint32 * 4),
-                ("rb_pieces", C.c_uint32 * 4), ("rb_entries", C.c_uint32 * 4),
-                ("rb_tiles", C.c_uint32 * 4), ("rb_work_items", C.c_uint32 * 4)]
+                ("rb_rows", C.c_uint32 * 5), ("rb_items", C.c_uint32 * 5),
+                ("rb_pieces", C.c_uint32 * 5), ("rb_entries", C.c_uint32 * 5),
+                ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5)]
 
     def as_dict(self):
         d = {}
@@ -78,7 +78,7 @@ class EvalStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-ABI_VERSION = 2  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 3  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [

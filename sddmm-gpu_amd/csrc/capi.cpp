@@ -130,8 +130,8 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
     s->col_reorder_ms = p.col_ms;
     s->dense_items = p.nDenseItems;
     s->residual_items = p.nResItems;
-    for (int i = 0; i < 4; ++i) {  // per row size: the fp32 layout, else the fp16/bf16 one
-        const Plan::RowBlockLayout& L = p.rbl[i].rowBytes ? p.rbl[i] : p.rbl[i + 4];
+    for (int i = 0; i < Plan::N_RB_SIZES; ++i) {  // per row size: the fp32 layout, else the half one
+        const Plan::RowBlockLayout& L = p.rbl[i].rowBytes ? p.rbl[i] : p.rbl[i + Plan::N_RB_SIZES];
         s->rb_rows[i] = L.rowBytes ? L.RB : 0;
         s->rb_items[i] = L.rowBytes ? L.nItems : 0;
         s->rb_pieces[i] = L.rowBytes ? L.nPieces : 0;

@@ -916,7 +916,8 @@ const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, bool half, u32 p
     *err = BSMR_OK;
     const u32 tmin = half ? tile_min_half : tile_min_f32;
     if (pa == 0 && pb == P) {
-        const int slot = (rowBytes == 256 ? 0 : rowBytes == 512 ? 1 : rowBytes == 1024 ? 2 : 3) + (half ? 4 : 0);
+        const int slot = (rowBytes == 128 ? 0 : rowBytes == 256 ? 1 : rowBytes == 512 ? 2 : rowBytes == 1024 ? 3 : 4) +
+                         (half ? Plan::N_RB_SIZES : 0);
         RowBlockLayout& L = rbl[slot];
         if (L.rowBytes != rowBytes || L.tileMin != tmin)
             *err = build_rowblock_layout(L, rowBytes, 0, P, tmin);
@@ -1191,7 +1192,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // [ph NG, (ph + 1) NG). Longest first, so the 16 row-groups of a wave get pieces of similar
     // length: over the whole item (piece_order 0), or inside column windows of one phase
     // (piece_order 1: all items of an XCD would sweep their column range together)
-    const u32 G = rowBytes >= 2048 ? 16 : rowBytes >= 1024 ? 8 : 4;  // sddmm.hip RowGeom
+    const u32 G = rowBytes >= 2048 ? 16 : rowBytes >= 1024 ? 8 : 4;  // sddmm.hip RowGeom (128..512: 4)
     const u32 NG = piece_order == 1 ? NT / G : 0xFFFFFFFFu;  // sort window
     std::vector<uint2> pieces;
     pieces.reserve(n / 4 + items.size());

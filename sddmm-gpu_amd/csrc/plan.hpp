@@ -108,8 +108,9 @@ struct Plan {
         // shard cost model of bsmr_plan_shard
         std::vector<double> rbCost;
     };
-    // rows of 256, 512, 1024 and 2048 bytes, for fp32 [0, 4) and fp16/bf16 [4, 8) (tileMin)
-    static constexpr int N_RB_LAYOUTS = 8;
+    // rows of 128, 256, 512, 1024 and 2048 bytes, for fp32 [0, 5) and fp16/bf16 [5, 10) (tileMin)
+    static constexpr int N_RB_SIZES = 5;
+    static constexpr int N_RB_LAYOUTS = 2 * N_RB_SIZES;
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
     // stored entries a dense tile needs to run on MFMA in the row-block launch (BSMR_TILE_MIN_F32
     // / BSMR_TILE_MIN_HALF); 0 = every tile. Measured (r01k sweep, profiles/r01k/tile_min.json):

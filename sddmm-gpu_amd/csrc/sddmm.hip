@@ -513,7 +513,10 @@ struct DenseTileLds {
     static constexpr int CH = NK > 8 ? 8 : NK;   // chunks held in registers at once
     u32 lr, c, idx[4];
     __device__ __forceinline__ static u32 chunk(int kk, u32 g) {
-        return 16 * (kk >> 2) + 4 * g + (kk & 3);
+        if constexpr (NK >= 4)
+            return 16 * (kk >> 2) + 4 * g + (kk & 3);
+        else  // 128-byte rows: k-step kk covers chunks kk, NK + kk, 2 NK + kk, 3 NK + kk
+            return NK * g + kk;
     }
     __device__ __forceinline__ void meta(const RbArgs& a, const u32 tile, const u32 q0) {
         const u32 l = __lane_id(), rr = l & 15, g = l >> 4;
@@ -697,31 +700,49 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
         constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
         static_assert(MAXB * NW == (NT == 1024 ? 160u : 80u), "whole KiB blocks");
-        static_assert(MAXB * NR <= 64, "one row index per lane");
         const u32 lane = tid & 63;
         const u32 ws = __builtin_amdgcn_readfirstlane(w);  // wave index in an SGPR
-        u32 rowv = 0;
-        {
-            const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
-            if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
-        }
         // the source chunk of lane l is the same in every block of the wave: x % NCH and
-        // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 16)
+        // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
         const u32 x0 = 64 * ws + lane;
         const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
-#pragma unroll
-        for (u32 i = 0; i < MAXB; ++i) {
-            const u32 b = ws + i * NW;
-            u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
-#pragma unroll
-            for (u32 k = 1; k < NR; ++k) {
-                const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
-                src = lane / NCH == k ? rk : src;
+        if constexpr (MAXB * NR <= 64) {
+            u32 rowv = 0;
+            {
+                const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
+                if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
             }
-            const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                             (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                             16, 0, 0);
+#pragma unroll
+            for (u32 i = 0; i < MAXB; ++i) {
+                const u32 b = ws + i * NW;
+                u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
+#pragma unroll
+                for (u32 k = 1; k < NR; ++k) {
+                    const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
+                    src = lane / NCH == k ? rk : src;
+                }
+                const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
+                                                 16, 0, 0);
+            }
+        } else {
+            // 128-byte rows: 8 rows per block, too many indices for one per lane; each lane loads
+            // the row of its own chunk for every block (all loads first, then the LDS-DMAs)
+            u32 src[MAXB];
+#pragma unroll
+            for (u32 i = 0; i < MAXB; ++i) {
+                const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
+                src[i] = lr < a.RB && q < a.R ? a.rows[q] : 0u;
+            }
+#pragma unroll
+            for (u32 i = 0; i < MAXB; ++i) {
+                const u32 b = ws + i * NW;
+                const char* g = a.A + (static_cast<size_t>(src[i]) * RBY + coff);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
+                                                 16, 0, 0);
+            }
         }
     }
     __syncthreads();
@@ -835,7 +856,7 @@ int rb_slot(const Plan& p, u32 K, int dtype) {
     if (!p.force_rowblock && static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16)
         return -1;
     const u32 rby = K * (dtype == BSMR_F32 ? 4u : 2u);
-    return rby == 256 ? 0 : rby == 512 ? 1 : rby == 1024 ? 2 : rby == 2048 ? 3 : -1;
+    return rby == 128 ? 0 : rby == 256 ? 1 : rby == 512 ? 2 : rby == 1024 ? 3 : rby == 2048 ? 4 : -1;
 }
 
 // the row-block layout of panels [pa, pb) for slot's row size (built on first use)
@@ -843,7 +864,7 @@ int get_rb_layout(const Plan& p, int slot, int dtype, u32 pa, u32 pb,
                   const Plan::RowBlockLayout** out) {
     std::lock_guard<std::mutex> g(p.layout_mu);
     int err = BSMR_OK;
-    *out = p.rowblock_layout(256u << slot, dtype != BSMR_F32, pa, pb, &err);
+    *out = p.rowblock_layout(128u << slot, dtype != BSMR_F32, pa, pb, &err);
     return err;
 }
 
@@ -881,7 +902,8 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     void (*fn)(RbArgs) = nullptr;
 #define BSMR_RB(DT, RBY) (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>)
 #define BSMR_RB2(DT)                                                                   \
-    (L.rowBytes == 256    ? BSMR_RB(DT, 256)                                              \
+    (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
+     : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
      : L.rowBytes == 512  ? BSMR_RB(DT, 512)                                              \
      : L.rowBytes == 1024 ? BSMR_RB(DT, 1024)                                             \
                           : BSMR_RB(DT, 2048))
