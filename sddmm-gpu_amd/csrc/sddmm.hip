@@ -568,7 +568,7 @@ template <int RBY>
 __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const u32 sub,
                                           const u32 (&rot)[RowGeom<RBY>::NC],
                                           f32x4 (&bv)[RowGeom<RBY>::NC]) {
-    const u32 bb = col * RBY + 16 * sub;
+    const u32 bb = col * RBY + 16 * sub;  // B < 4 GiB on this path (rb_slot)
 #pragma unroll
     for (u32 f = 0; f < RowGeom<RBY>::NC; ++f) bv[f] = ld16(a.B + (bb + rot[f]));
 }
@@ -856,6 +856,8 @@ int rb_slot(const Plan& p, u32 K, int dtype) {
     if (!p.force_rowblock && static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16)
         return -1;
     const u32 rby = K * (dtype == BSMR_F32 ? 4u : 2u);
+    // the row-block kernel addresses B with 32-bit byte offsets (load_bcol): B < 4 GiB
+    if (static_cast<u64>(p.N) * rby >= (1ull << 32)) return -1;
     return rby == 128 ? 0 : rby == 256 ? 1 : rby == 512 ? 2 : rby == 1024 ? 3 : rby == 2048 ? 4 : -1;
 }
 
