@@ -71,6 +71,7 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     if (const char* tm = std::getenv("BSMR_TILE_MIN_HALF")) p.tile_min_half = static_cast<u32>(std::atoi(tm));
     if (const char* pm = std::getenv("BSMR_PIECE_MAX"))
         p.piece_max = std::min<u32>(RB_PIECE_MAX, std::max(1, std::atoi(pm)));
+    if (const char* dm = std::getenv("BSMR_DENSE_MIN")) p.dense_min = static_cast<float>(std::atof(dm));
     if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
         p.l2_range_kb = std::max(64, std::atoi(l2));
     u64 free_mem = o.free_mem_bytes;

@@ -20,6 +20,9 @@ struct Plan;
 // fp16/bf16 SDDMM launch (sddmm_half.hip); mode: 1 dense tiles, 2 residual, 3 both
 int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
                 u32 mode, hipStream_t s, u32 nb = 1);
+// fp16/bf16 dense-sampled launch (sddmm_dense.hip): K a multiple of 128
+int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
+                 hipStream_t s, u32 nb = 1);
 
 u32 block_size_for(u32 M, u32 N, u64 free_mem);
 u32 cluster_block_dim(u32 nbpr);
@@ -45,6 +48,10 @@ struct Plan {
     u32 l2_range_kb = 2048;
     // entries per column-run piece of the row-block layout (<= RB_PIECE_MAX; BSMR_PIECE_MAX)
     u32 piece_max = RB_PIECE_MAX;
+    // fp16/bf16 patterns with at least this fraction of M x N stored run the dense-sampled
+    // launch (whole 128 x 128 MFMA tiles; BSMR_DENSE_MIN; > 1 = never). Measured crossover
+    // (tools/dense_sweep.py, 2048^2 bf16 K=512): gathered faster at 3 %, dense from 5 %
+    float dense_min = 0.05f;
     // clusters per persistent clustering launch (bsmr_plan_options.cluster_batch); r01k timing
     // on reddit_like x0.25: 512 -> 9.7 s, 4096 -> 4.6 s, 16384 -> 2.3 s (fewer host round trips, more in flight)
     u32 cluster_batch = 16384;
@@ -137,6 +144,15 @@ struct Plan {
         return BSMR_OK;
     }
     mutable std::mutex layout_mu;
+
+    // dense-sampled launch: per 128 x 128 tile of P (original index space) its stored entries
+    struct DenseLayout {
+        bool built = false;
+        u32 ntn = 0, ntiles = 0;
+        DevBuf<u32> off, loc, out;  // loc = local row << 7 | local column; out = CSR position
+    };
+    mutable DenseLayout dense;
+    int build_dense_layout() const;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);
     int build_columns();

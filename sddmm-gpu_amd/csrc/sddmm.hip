@@ -861,6 +861,15 @@ int rb_slot(const Plan& p, u32 K, int dtype) {
     return rby == 128 ? 0 : rby == 256 ? 1 : rby == 512 ? 2 : rby == 1024 ? 3 : rby == 2048 ? 4 : -1;
 }
 
+// fp16/bf16 patterns dense enough for whole MFMA tiles (sddmm_dense.hip)
+bool use_dense(const Plan& p, u32 K, int dtype) {
+    // layout auto only (BSMR_LAYOUT_ROWBLOCK / _COLMAJOR force those launches)
+    // not for tile-dominated plans (16 x 16 block masks: the column-major tile launch)
+    if (static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16) return false;
+    return p.use_rowblock && !p.force_rowblock && dtype != BSMR_F32 && K % 128 == 0 &&
+           static_cast<double>(p.nnz) >= static_cast<double>(p.dense_min) * p.M * static_cast<double>(p.N);
+}
+
 // the row-block layout of panels [pa, pb) for slot's row size (built on first use)
 int get_rb_layout(const Plan& p, int slot, int dtype, u32 pa, u32 pb,
                   const Plan::RowBlockLayout** out) {
@@ -982,6 +991,10 @@ extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const
         const char* A = static_cast<const char*>(dA) + es * b0 * static_cast<size_t>(p.M) * K;
         const char* B = static_cast<const char*>(dB) + es * b0 * static_cast<size_t>(p.N) * K;
         float* P = dP + static_cast<size_t>(b0) * p.nnz;
+        if (use_dense(p, K, dtype)) {
+            BSMR_CHECK(launch_dense(p, A, B, K, dtype, P, s, nb));
+            continue;
+        }
         const int slot = rb_slot(p, K, dtype);
         if (slot >= 0) {
             const Plan::RowBlockLayout* L = nullptr;
@@ -1077,7 +1090,9 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     dense.nslots = 0;
     SddmmArgs res = full;
     res.nd = 0;
+    const bool dense_all = use_dense(p, K, dtype);
     auto run = [&](u32 mode) -> int {
+        if (dense_all) return launch_dense(p, dA, dB, K, dtype, dP, s);  // no dense/residual split
         if (L) return launch_rb(p, *L, dA, dB, dP, dtype, mode, s);
         if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, mode, s);
         return launch_full(p, mode == 1 ? dense : mode == 2 ? res : full, s);

@@ -65,6 +65,35 @@ def test_half_inputs_checkdata(dtype, K, case, layout):
     assert O.check_data(ref, P) == 0
 
 
+@pytest.mark.parametrize("case,K,dtype,force", [
+    ("uniform300", 256, F16, False),    # 20 % dense, ragged tiles (300 = 2 x 128 + 44)
+    ("uniform300", 128, BF16, False),
+    ("uniform300", 512, F16, False),
+    ("zipf", 128, BF16, True),          # sparse pattern forced dense: empty tiles skipped
+    ("zipf", 256, F16, True),
+])
+def test_dense_sampled_half(monkeypatch, case, K, dtype, force):
+    """The dense-sampled MFMA launch (whole 128 x 128 tiles of A B^T, sampled) for fp16/bf16
+    patterns above the density threshold (layout auto), against the oracle on the rounded
+    values."""
+    if force:
+        monkeypatch.setenv("BSMR_DENSE_MIN", "0")
+    if case == "uniform300":
+        M, N, rp, ci = synth.uniform_mask(300, 0.2, seed=5)
+    elif case == "zipf":
+        M, N, rp, ci = synth.random_rows(400, 3000, 50, seed=8, zipf=1.1)
+    else:
+        M, N, rp, ci = synth.block_mask(512, 16, 0.1, seed=7)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    conv = to_bf16_bits if dtype == BF16 else to_f16_bits
+    Ab, Ar = conv(make_data(M * K))
+    Bb, Br = conv(make_data(N * K)[::-1].copy())
+    P = run_half(plan, Ab, Bb, K, len(ci), dtype)
+    assert np.isfinite(P).all()
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, Ar, Br)
+    assert O.check_data(ref, P) == 0
+
+
 def test_dlmc_like_bf16_k512():
     M, N, rp, ci = synth.uniform_mask(2048, 0.1, seed=7)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
