@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "sddmm-gpu_amd"))
 
 METRIC = "SDDMM GFLOP/s (2·nnz·K) + HBM GB/s %peak, K=128, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+MFMA_HALF_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
 
 
 def parse():
@@ -340,6 +341,22 @@ def main():
         kern = f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)"
     else:
         kern = f"k_sddmm_half<{'f16' if dtype == 1 else 'bf16'}> (dense-tile MFMA + residual)"
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kern,
+            "bytes_alg_per_launch": bytes_alg}
+    dtiles = st_after.get("dense_sampled_tiles", 0)
+    if dtiles:  # sddmm.hip use_dense: whole 128 x 128 tiles on the matrix cores
+        kern = (f"k_sddmm_dense<{'f16' if dtype == 1 else 'bf16'},64,2> (dense-sampled: {dtiles} "
+                "non-empty 128 x 128 MFMA tiles, K in 64-wide LDS-DMA chunks, stored entries "
+                "sampled from the fp32 tile)")
+        flops_tiles = 2.0 * dtiles * 128 * 128 * K
+        ach = flops_tiles / (ms_per_step * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_HALF_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(ach / MFMA_HALF_PEAK_TFS, 4), "traffic": traffic,
+                "kernel": kern, "flops_alg_per_launch": flops_tiles,
+                "hbm_bytes_alg_per_launch": bytes_alg,
+                "note": "algorithmic FLOPs of the tiles computed (the dense-sampled launch "
+                        "computes every product of a non-empty tile)"}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -364,16 +381,7 @@ def main():
             "col_reorder_ms": round(st["col_reorder_ms"], 3), "b_broadcast_ms": round(bcast_ms, 3),
             "rowblock_layout": {k: st_after[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "kernel": kern,
-            "bytes_alg_per_launch": bytes_alg,
-        },
+        "roofline": roof,
         "kernels_ms": {k: round(v, 5) for k, v in prof.items()},
     }
     if kern.startswith("k_sddmm_rb"):

@@ -22,7 +22,8 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 3  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes) */
+#define BSMR_ABI_VERSION 4  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+                              4: dense_sampled_tiles */
 
 typedef enum {
     BSMR_OK = 0,
@@ -127,6 +128,9 @@ typedef struct {
     /* the same layouts: residual entries (incl. entries of demoted tiles), MFMA tiles kept,
      * non-padding items */
     uint32_t rb_entries[5], rb_tiles[5], rb_work_items[5];
+    /* fp16/bf16 dense-sampled launch (whole 128 x 128 MFMA tiles of P, patterns >= 5 % dense):
+     * tiles holding at least one stored entry, 0 = not built */
+    uint32_t dense_sampled_tiles;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

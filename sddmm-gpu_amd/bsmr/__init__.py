@@ -59,7 +59,8 @@ class PlanStats(C.Structure):
                 ("dense_items", C.c_uint32), ("residual_items", C.c_uint32),
                 ("rb_rows", C.c_uint32 * 5), ("rb_items", C.c_uint32 * 5),
                 ("rb_pieces", C.c_uint32 * 5), ("rb_entries", C.c_uint32 * 5),
-                ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5)]
+                ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5),
+                ("dense_sampled_tiles", C.c_uint32)]
 
     def as_dict(self):
         d = {}
@@ -78,7 +79,7 @@ class EvalStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-ABI_VERSION = 3  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 4  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [

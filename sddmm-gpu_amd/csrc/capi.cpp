@@ -140,6 +140,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_tiles[i] = L.rowBytes ? L.nTilesKept : 0;
         s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
     }
+    s->dense_sampled_tiles = p.dense.built ? p.dense.nonempty : 0;
     return BSMR_OK;
 }
 

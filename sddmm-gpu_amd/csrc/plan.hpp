@@ -20,7 +20,7 @@ struct Plan;
 // fp16/bf16 SDDMM launch (sddmm_half.hip); mode: 1 dense tiles, 2 residual, 3 both
 int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
                 u32 mode, hipStream_t s, u32 nb = 1);
-// fp16/bf16 dense-sampled launch (sddmm_dense.hip): K a multiple of 128
+// fp16/bf16 dense-sampled launch (sddmm_dense.hip): K a multiple of 64
 int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
                  hipStream_t s, u32 nb = 1);
 
@@ -148,7 +148,7 @@ struct Plan {
     // dense-sampled launch: per 128 x 128 tile of P (original index space) its stored entries
     struct DenseLayout {
         bool built = false;
-        u32 ntn = 0, ntiles = 0;
+        u32 ntn = 0, ntiles = 0, nonempty = 0;
         DevBuf<u32> off, loc, out;  // loc = local row << 7 | local column; out = CSR position
     };
     mutable DenseLayout dense;

@@ -866,7 +866,7 @@ bool use_dense(const Plan& p, u32 K, int dtype) {
     // layout auto only (BSMR_LAYOUT_ROWBLOCK / _COLMAJOR force those launches)
     // not for tile-dominated plans (16 x 16 block masks: the column-major tile launch)
     if (static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16) return false;
-    return p.use_rowblock && !p.force_rowblock && dtype != BSMR_F32 && K % 128 == 0 &&
+    return p.use_rowblock && !p.force_rowblock && dtype != BSMR_F32 && K % 64 == 0 &&
            static_cast<double>(p.nnz) >= static_cast<double>(p.dense_min) * p.M * static_cast<double>(p.N);
 }
 

@@ -5,8 +5,9 @@
 // Tile (tm, tn) = rows [128 tm, +128) x columns [128 tn, +128) of P = A B^T in the ORIGINAL index
 // space (the reordering does not change which dot products exist). One 256-thread workgroup per
 // non-empty tile: the K loop streams 64-wide k-chunks of the tile's 128 A rows and 128 B rows
-// (128 bytes each) into LDS by LDS-DMA, double-buffered in two static images so a chunk's
-// LDS-DMA is in flight while the previous chunk's MFMAs run; wave (wy, wx) owns a 64 x 64 quadrant as
+// (128 bytes each) into LDS by LDS-DMA through a ring of NS stages (NS - 1 chunks in flight while
+// one computes; NS = 2 fits two workgroups per CU, so one tile's prologue and epilogue overlap
+// another's MFMAs); wave (wy, wx) owns a 64 x 64 quadrant as
 // 4 x 4 `v_mfma_f32_16x16x32_{f16,bf16}` accumulators (fp32). The finished tile goes through LDS
 // (fp32) and the workgroup writes exactly the tile's stored entries to P, in CSR order positions
 // (Plan::DenseLayout: per-tile entry lists of local row << 7 | local column and output index).
@@ -26,9 +27,9 @@ typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
 
 constexpr u32 DT_TILE = 128;   // output tile edge
-constexpr u32 DT_KC = 64;      // k-chunk per barrier (two MFMA k-steps of 32)
-constexpr u32 DT_CHUNK = DT_TILE * DT_KC * 2;  // bytes of one operand chunk image (16 KiB)
-constexpr u32 DT_CS = DT_TILE + 4;             // fp32 output image row stride (floats)
+// k-chunk per barrier KC: 64 (two MFMA k-steps of 32; 128-byte rows) or 32 (one; 64-byte rows)
+template <u32 KC>
+constexpr u32 chunk_bytes() { return DT_TILE * KC * 2; }  // one operand chunk image
 
 struct DenseArgs {
     const char* A;  // M x K halves, row-major
@@ -41,34 +42,42 @@ struct DenseArgs {
     unsigned long long bA, bB, bP;  // batched launch: A/B byte strides, P element stride
 };
 
-__shared__ __attribute__((aligned(16))) char g_da0[DT_CHUNK];
-__shared__ __attribute__((aligned(16))) char g_db0[DT_CHUNK];
-__shared__ __attribute__((aligned(16))) char g_da1[DT_CHUNK];
-__shared__ __attribute__((aligned(16))) char g_db1[DT_CHUNK];
-__shared__ __attribute__((aligned(16))) float g_dc[DT_TILE * DT_CS];
+// 16-byte slot of (row r, k-group g) in a chunk image of KC/8 groups per row: the groups of a
+// row permuted by a row-dependent XOR so the 16 lanes of each ds_read_b128 lane group (rows
+// l & 15, one group) hit 16 distinct 16-byte bank groups
+template <u32 KC>
+__device__ __forceinline__ u32 dswz(u32 r) {
+    return KC == 64 ? (r >> 1) & 7 : (r >> 2) & 3;
+}
+template <u32 KC>
+__device__ __forceinline__ u32 dslot(u32 r, u32 g) { return (KC / 8) * r + (g ^ dswz<KC>(r)); }
 
-// 16-byte slot of (row r, k-group g < 8) in a chunk image: rows of 128 bytes, the eight groups of
-// a row permuted by (r >> 1) & 7, so the 16 lanes of each ds_read_b128 lane group (rows l & 15,
-// group 4 s + (l >> 4)) hit 16 distinct 16-byte bank groups
-__device__ __forceinline__ u32 dslot(u32 r, u32 g) { return 8 * r + (g ^ ((r >> 1) & 7)); }
+// one wave-wide 16-byte-per-lane LDS-DMA (lane l lands at l*16 past the wave-uniform l).
+// Issued by inline asm on purpose: the compiler's wait-count pass loses track of LDS-DMA
+// stores across the k-loop's back edge and would put a vmcnt(0) at its head; these DMAs are
+// instead ordered by the kernel's own vmcnt waits + barriers.
+__device__ __forceinline__ void lds_dma16(const char* g, char* l) {
+    const u32 m0 = __builtin_amdgcn_readfirstlane(static_cast<u32>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)l)));
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
+                 : "memory", "m0");
+}
 
-// chunk kc of the tile's A and B rows into (sa, sb): 1024 slots each, 4 LDS-DMAs per wave and
-// operand, no branches (rows past M / N read the last row; they are never sampled)
+// chunk kc of the tile's A and B rows into (sa, sb): KC/16 LDS-DMAs per wave and operand, no
+// branches (rows past M / N read the last row; they are never sampled)
+template <u32 KC>
 __device__ __forceinline__ void dense_stage(const DenseArgs& a, const u32 r0, const u32 c0,
                                             const u32 kc, const u32 ws, const u32 lane, char* sa,
                                             char* sb) {
+    constexpr u32 ND = KC / 16, GP = KC / 8;
     const size_t rowB = static_cast<size_t>(a.K) * 2;
 #pragma unroll
-    for (u32 i = 0; i < 4; ++i) {
-        const u32 s = 64 * (4 * ws + i) + lane, r = s >> 3, g = (s & 7) ^ ((r >> 1) & 7);
+    for (u32 i = 0; i < ND; ++i) {
+        const u32 s = 64 * (ND * ws + i) + lane, r = s / GP, g = (s % GP) ^ dswz<KC>(r);
         const u32 ra = min(r0 + r, a.M - 1), rb = min(c0 + r, a.N - 1);
-        const size_t ko = static_cast<size_t>(kc) * (DT_KC * 2) + 16 * g;
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(a.A + ra * rowB + ko),
-            (__attribute__((address_space(3))) void*)(sa + 1024 * (4 * ws + i)), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(a.B + rb * rowB + ko),
-            (__attribute__((address_space(3))) void*)(sb + 1024 * (4 * ws + i)), 16, 0, 0);
+        const size_t ko = static_cast<size_t>(kc) * (KC * 2) + 16 * g;
+        lds_dma16(a.A + ra * rowB + ko, sa + 1024 * (ND * ws + i));
+        lds_dma16(a.B + rb * rowB + ko, sb + 1024 * (ND * ws + i));
     }
 }
 
@@ -83,18 +92,18 @@ __device__ __forceinline__ f32x4 mfma16x16x32(const f32x4 x, const f32x4 y, cons
 }
 
 // one k-chunk of the wave's 64 x 64 quadrant from the images (sa, sb)
-template <int DT>
+template <int DT, u32 KC>
 __device__ __forceinline__ void dense_chunk(const char* sa, const char* sb, const u32 wy,
                                             const u32 wx, const u32 lane, f32x4 (&acc)[4][4]) {
     const u32 rr = lane & 15, g4 = lane >> 4;
 #pragma unroll
-    for (u32 ks = 0; ks < DT_KC / 32; ++ks) {
+    for (u32 ks = 0; ks < KC / 32; ++ks) {
         f32x4 av[4], bv[4];
 #pragma unroll
         for (u32 i = 0; i < 4; ++i) {
             const u32 ra = 64 * wy + 16 * i + rr, rb = 64 * wx + 16 * i + rr;
-            av[i] = *reinterpret_cast<const f32x4*>(sa + 16 * dslot(ra, 4 * ks + g4));
-            bv[i] = *reinterpret_cast<const f32x4*>(sb + 16 * dslot(rb, 4 * ks + g4));
+            av[i] = *reinterpret_cast<const f32x4*>(sa + 16 * dslot<KC>(ra, 4 * ks + g4));
+            bv[i] = *reinterpret_cast<const f32x4*>(sb + 16 * dslot<KC>(rb, 4 * ks + g4));
         }
 #pragma unroll
         for (u32 i = 0; i < 4; ++i)
@@ -103,8 +112,21 @@ __device__ __forceinline__ void dense_chunk(const char* sa, const char* sb, cons
     }
 }
 
-template <int DT>
-__global__ __launch_bounds__(256) void k_sddmm_dense(DenseArgs a) {
+template <u32 KC, u32 NS>
+constexpr u32 dense_lds() { return NS * 2 * chunk_bytes<KC>(); }
+// workgroups per CU the LDS allows (160 KiB), capped at 4 (VGPR budget 128)
+template <u32 KC, u32 NS>
+constexpr u32 dense_wgs() { return 160u * 1024 / dense_lds<KC, NS>() < 4 ? 160u * 1024 / dense_lds<KC, NS>() : 4; }
+
+template <int DT, u32 KC, u32 NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dense_wgs<KC, NS>())))
+void k_sddmm_dense(DenseArgs a) {
+    constexpr u32 CB = chunk_bytes<KC>(), LDS = dense_lds<KC, NS>();
+    // NS stages of (A chunk, B chunk) images; the finished fp32 tile passes through the same
+    // bytes, CR rows (of 512 bytes) at a time
+    constexpr u32 CR = LDS >= DT_TILE * 512 ? DT_TILE : 64;  // passes of whole wave rows
+    static_assert(LDS >= CR * 512, "the epilogue pass fits the stage images");
+    __shared__ __attribute__((aligned(16))) char st[LDS];
     if (blockIdx.y) {
         a.A += blockIdx.y * a.bA;
         a.B += blockIdx.y * a.bB;
@@ -125,32 +147,48 @@ __global__ __launch_bounds__(256) void k_sddmm_dense(DenseArgs a) {
     for (u32 i = 0; i < 4; ++i)
 #pragma unroll
         for (u32 jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const u32 nk = a.K / DT_KC;  // even (launch_dense: K a multiple of 128)
-    dense_stage(a, r0, c0, 0, ws, lane, g_da0, g_db0);
-    __syncthreads();
-    for (u32 kc = 0; kc < nk; kc += 2) {
-        // chunk kc + 1 lands in image 1 while chunk kc computes from image 0, and so on; the
-        // last prefetch re-reads chunk nk - 1 (no branch around an LDS-DMA)
-        dense_stage(a, r0, c0, kc + 1, ws, lane, g_da1, g_db1);
-        dense_chunk<DT>(g_da0, g_db0, wy, wx, lane, acc);
-        __syncthreads();
-        dense_stage(a, r0, c0, min(kc + 2, nk - 1), ws, lane, g_da0, g_db0);
-        dense_chunk<DT>(g_da1, g_db1, wy, wx, lane, acc);
-        __syncthreads();
+    const u32 nk = a.K / KC;  // launch_dense: K a multiple of KC
+    // chunk kc lands in stage kc % NS. Before a stage is read every wave waits for its own
+    // LDS-DMAs into it (KC/8 per stage; those of the NS - 2 younger stages may stay in flight)
+    // and the workgroup barrier then makes everyone's visible; the same barrier ends all reads
+    // of the stage the next prefetch overwrites. Prefetches past the last chunk re-read it (no
+    // branch around an LDS-DMA).
+    auto stage = [&](const u32 kc) {
+        char* const sa = st + (kc % NS) * (2 * CB);
+        dense_stage<KC>(a, r0, c0, min(kc, nk - 1), ws, lane, sa, sa + CB);
+    };
+#pragma unroll
+    for (u32 j = 0; j + 1 < NS; ++j) stage(j);
+    for (u32 kc = 0; kc < nk; ++kc) {
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(KC / 8 * (NS - 2)) : "memory");
+        stage(kc + NS - 1);
+        const char* const sa = st + (kc % NS) * (2 * CB);
+        dense_chunk<DT, KC>(sa, sa + CB, wy, wx, lane, acc);
     }
-    // accumulator (i, jj) reg r of lane l = D[64 wy + 16 i + 4 (l >> 4) + r][64 wx + 16 jj + (l & 15)]
+    // every read done, every LDS-DMA (the clamped tail prefetches too) landed: the images
+    // become the fp32 tile
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    float* const ct = reinterpret_cast<float*>(st);
+    // accumulator (i, jj) reg r of lane l = D[64 wy + 16 i + 4 (l >> 4) + r][64 wx + 16 jj + (l & 15)];
+    // pass h holds tile rows [CR h, CR h + CR)
 #pragma unroll
-    for (u32 i = 0; i < 4; ++i)
+    for (u32 h = 0; h < DT_TILE / CR; ++h) {
+        if (h) __syncthreads();  // the previous pass's reads are done
+        if (CR == DT_TILE || wy == h) {
 #pragma unroll
-        for (u32 jj = 0; jj < 4; ++jj)
+            for (u32 i = 0; i < 4; ++i)
 #pragma unroll
-            for (u32 r = 0; r < 4; ++r)
-                g_dc[(64 * wy + 16 * i + 4 * (lane >> 4) + r) * DT_CS + 64 * wx + 16 * jj + (lane & 15)] =
-                    acc[i][jj][r];
-    __syncthreads();
-    for (u32 e = e0 + tid; e < e1; e += 256) {
-        const u32 lc = a.loc[e];
-        a.P[a.out[e]] = g_dc[(lc >> 7) * DT_CS + (lc & 127)];
+                for (u32 jj = 0; jj < 4; ++jj)
+#pragma unroll
+                    for (u32 r = 0; r < 4; ++r)
+                        ct[(64 * wy + 16 * i + 4 * (lane >> 4) + r - CR * h) * DT_TILE + 64 * wx +
+                           16 * jj + (lane & 15)] = acc[i][jj][r];
+        }
+        __syncthreads();
+        for (u32 e = e0 + tid; e < e1; e += 256) {
+            const u32 lc = a.loc[e] - CR * DT_TILE * h;  // loc = local row * 128 + local column
+            if (lc < CR * DT_TILE) a.P[a.out[e]] = ct[lc];
+        }
     }
 }
 
@@ -182,11 +220,13 @@ int Plan::build_dense_layout() const {
     BSMR_HIP(hipStreamSynchronize(stream));
     D.ntn = ntn;
     D.ntiles = static_cast<u32>(ntiles);
+    D.nonempty = 0;
+    for (size_t t = 0; t < ntiles; ++t) D.nonempty += off[t + 1] > off[t];
     D.built = true;
     return BSMR_OK;
 }
 
-// fp16/bf16, K a multiple of 128: the whole product in 128 x 128 MFMA tiles, sampled
+// fp16/bf16, K a multiple of 64: the whole product in 128 x 128 MFMA tiles, sampled
 int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
                  hipStream_t s, u32 nb) {
     {
@@ -211,10 +251,14 @@ int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     a.bP = p.nnz;
     const u32 per = (D.ntiles + XCD_BUCKETS - 1) / XCD_BUCKETS;
     const u32 grid = per * XCD_BUCKETS;
+    const dim3 g(grid, nb);
+    // (KC, NS) = (64, 2): two workgroups per CU. Measured (tools/gpu_dense_stages.sh history,
+    // r01q): 4 stages at one workgroup per CU and KC = 32 at 2-4 stages / 2-4 workgroups were
+    // all slower (C5 uniform 10.6-12.1 us vs 8.8-9.8)
     if (dtype == BSMR_F16)
-        hipLaunchKernelGGL(k_sddmm_dense<1>, dim3(grid, nb), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2>), g, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(k_sddmm_dense<2>, dim3(grid, nb), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2>), g, dim3(256), 0, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }

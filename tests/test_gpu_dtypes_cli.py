@@ -69,6 +69,8 @@ def test_half_inputs_checkdata(dtype, K, case, layout):
     ("uniform300", 256, F16, False),    # 20 % dense, ragged tiles (300 = 2 x 128 + 44)
     ("uniform300", 128, BF16, False),
     ("uniform300", 512, F16, False),
+    ("uniform300", 64, F16, False),     # one k-chunk: every prefetch re-reads it
+    ("uniform300", 320, BF16, False),   # 5 chunks: the 4-stage loop leaves mid-way
     ("zipf", 128, BF16, True),          # sparse pattern forced dense: empty tiles skipped
     ("zipf", 256, F16, True),
 ])
