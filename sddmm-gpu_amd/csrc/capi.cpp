@@ -72,6 +72,8 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     if (const char* pm = std::getenv("BSMR_PIECE_MAX"))
         p.piece_max = std::min<u32>(RB_PIECE_MAX, std::max(1, std::atoi(pm)));
     if (const char* dm = std::getenv("BSMR_DENSE_MIN")) p.dense_min = static_cast<float>(std::atof(dm));
+    if (const char* orr = std::getenv("BSMR_ORIG_ROWS"))  // "0" never, "1" always, else auto
+        p.orig_rows = orr[0] == '0' ? 0 : orr[0] == '1' ? 1 : -1;
     if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
         p.l2_range_kb = std::max(64, std::atoi(l2));
     u64 free_mem = o.free_mem_bytes;
@@ -132,7 +134,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
     s->dense_items = p.nDenseItems;
     s->residual_items = p.nResItems;
     for (int i = 0; i < Plan::N_RB_SIZES; ++i) {  // per row size: the fp32 layout, else the half one
-        const Plan::RowBlockLayout& L = p.rbl[i].rowBytes ? p.rbl[i] : p.rbl[i + Plan::N_RB_SIZES];
+        const Plan::RowBlockLayout& L = p.rbl[i].rowBytes ? p.rb_whole(i) : p.rb_whole(i + Plan::N_RB_SIZES);
         s->rb_rows[i] = L.rowBytes ? L.RB : 0;
         s->rb_items[i] = L.rowBytes ? L.nItems : 0;
         s->rb_pieces[i] = L.rowBytes ? L.nPieces : 0;
@@ -297,7 +299,7 @@ extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtyp
     // the same row blocks; otherwise the per-panel model of bsmr_shard_cuts
     const Plan::RowBlockLayout* L = nullptr;
     BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
-    if (L && L->nRB > 0) {
+    if (L && L->nRB > 0 && !L->orig) {  // (original-order row blocks do not map to panels)
         const u32 nRB = L->nRB, ppr = L->RB / 16;
         std::vector<double> cum(nRB + 1ull, 0.0);
         for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b];

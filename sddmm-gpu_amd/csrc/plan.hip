@@ -751,6 +751,20 @@ __global__ __launch_bounds__(256) void k_rb_keys(const u32* __restrict__ sdoff,
     }
 }
 
+// original-order row blocks: key = (row / RB) * N + col for every stored entry (thread per row)
+__global__ __launch_bounds__(256) void k_rb_keys_csr(const u32* __restrict__ rowptr,
+                                                     const u32* __restrict__ colidx, u32 M, u32 RB,
+                                                     u32 N, unsigned long long* __restrict__ keys,
+                                                     u32* __restrict__ vals, u32* __restrict__ qOf) {
+    const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= M) return;
+    for (u32 e = rowptr[r]; e < rowptr[r + 1]; ++e) {
+        keys[e] = static_cast<unsigned long long>(r / RB) * N + colidx[e];
+        vals[e] = e;
+        qOf[e] = r;
+    }
+}
+
 // stored entries of tiles [t0, t0 + gridDim.x) (one 256-thread block per tile)
 __global__ __launch_bounds__(256) void k_tile_nnz(const u32* __restrict__ blockValues, u32 t0,
                                                   u32* __restrict__ cnt) {
@@ -808,6 +822,21 @@ __global__ void k_rb_gather(const u32* __restrict__ order, const u32* __restrict
     const u32 q = qOf[e];
     meta[i] = ((q % RB) << 22) | (e < n0 ? sparseColIdx[e] : dcol[e - n0]);
     out[i] = e < n0 ? sparseValues[e] : dout[e - n0];
+    const u32 rb = q / RB;
+    if (i + 1 == n || qOf[order[i + 1]] / RB != rb) rbEnd[rb] = i + 1;
+}
+
+// k_rb_gather for original-order row blocks: entry e is CSR position e
+__global__ void k_rb_gather_csr(const u32* __restrict__ order, const u32* __restrict__ qOf,
+                                const u32* __restrict__ colidx, u32 n, u32 RB,
+                                u32* __restrict__ meta, u32* __restrict__ out,
+                                u32* __restrict__ rbEnd) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32 e = order[i];
+    const u32 q = qOf[e];
+    meta[i] = ((q % RB) << 22) | colidx[e];
+    out[i] = e;
     const u32 rb = q / RB;
     if (i + 1 == n || qOf[order[i + 1]] / RB != rb) rbEnd[rb] = i + 1;
 }
@@ -932,9 +961,35 @@ const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, bool half, u32 p
         const int slot = (rowBytes == 128 ? 0 : rowBytes == 256 ? 1 : rowBytes == 512 ? 2 : rowBytes == 1024 ? 3 : 4) +
                          (half ? Plan::N_RB_SIZES : 0);
         RowBlockLayout& L = rbl[slot];
-        if (L.rowBytes != rowBytes || L.tileMin != tmin)
+        if (L.rowBytes != rowBytes || L.tileMin != tmin) {
+            rb_use_orig[slot] = false;
             *err = build_rowblock_layout(L, rowBytes, 0, P, tmin);
-        return *err == BSMR_OK ? &L : nullptr;
+            if (*err != BSMR_OK) return nullptr;
+            // sparse rows (the same < 64 entries per row rule as the row-block sizing): try
+            // original-order row blocks and keep the cheaper layout by the shard cost model
+            const bool sparse = R && static_cast<u64>(nres) + static_cast<u64>(numDenseTiles) * 16 <
+                                         64ull * R;
+            if (orig_rows == 1 || (orig_rows != 0 && sparse)) {
+                RowBlockLayout& Lo = rblo[slot];
+                *err = build_rowblock_layout(Lo, rowBytes, 0, P, tmin, true);
+                if (*err != BSMR_OK) return nullptr;
+                // column-run pieces (one B row gathered each) and MFMA tiles decide: the entries
+                // are the same, and their LDS dot products cost far less than a gathered row
+                // (C3 cop20k-like: 1.03 M -> 0.80 M pieces, 109 -> 78 us)
+                const double c = L.nPieces + 16.0 * L.nTilesKept, co = Lo.nPieces;
+                rb_use_orig[slot] = orig_rows == 1 || co < 0.9 * c;
+                if (!rb_use_orig[slot]) {  // keep the decision, free the candidate
+                    Lo.meta.release();
+                    Lo.out.release();
+                    Lo.items.release();
+                    Lo.itemEnd.release();
+                    Lo.pieces.release();
+                    Lo.tileIds.release();
+                    Lo.rowIds.release();
+                }
+            }
+        }
+        return &rb_whole(slot);
     }
     for (const auto& L : shard_rbl)
         if (L->rowBytes == rowBytes && L->pa == pa && L->pb == pb && L->tileMin == tmin) return L.get();
@@ -947,20 +1002,27 @@ const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, bool half, u32 p
 }
 
 // Row-block launch layout over panels [pa, pb) (the whole plan, or one row-panel shard).
-int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin) const {
+int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
+                                bool orig) const {
     L.rowBytes = 0;
+    L.orig = orig;
     hipStream_t s = stream;
     if (N > (1u << 22)) {
         set_error("row-block layout needs N <= 2^22");
         return BSMR_ERR_UNSUPPORTED;
     }
-    const u32 qa = 16 * pa, qend = std::min(R, 16 * pb);
-    const u32 Rs = qend > qa ? qend - qa : 0;  // reordered rows of the range
+    if (orig && (pa != 0 || pb != P)) {
+        set_error("original-order row blocks cover the whole plan only");
+        return BSMR_ERR_INVALID;
+    }
+    const u32 qa = orig ? 0 : 16 * pa, qend = orig ? M : std::min(R, 16 * pb);
+    const u32 Rs = qend > qa ? qend - qa : 0;  // (reordered) rows of the range
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    const u32 ebase = h_sparseValueOffsets[pa];
-    const u32 n0 = h_sparseValueOffsets[pb] - ebase;  // residual entries of the range
+    const u32 ebase = orig ? 0 : h_sparseValueOffsets[pa];
+    // residual entries of the range (original order: every stored entry)
+    const u32 n0 = orig ? nnz : h_sparseValueOffsets[pb] - ebase;
     u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, Rs);
     {
         // sparse rows (< 64 stored entries per row: banded / FEM patterns) keep their row blocks
@@ -983,7 +1045,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 wgPerCU = NT == 1024 ? 1 : 2;
     const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
     // dense tiles of the range: kept (>= tileMin stored entries) or demoted to entries
-    const u32 T0 = h_blockOffsets[pa], nT = h_blockOffsets[pb] - T0;
+    const u32 T0 = h_blockOffsets[pa], nT = orig ? 0 : h_blockOffsets[pb] - T0;
     std::vector<u32> tcnt(nT, 0), doff(nT, NULLV), keptPos(nT + 1ull, 0), hkept;
     u32 nd = 0;
     if (nT && tileMin > 0) {
@@ -1024,7 +1086,10 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_CHECK(dcol.alloc(std::max<u32>(nd, 1)));
         BSMR_CHECK(dout.alloc(std::max<u32>(nd, 1)));
         BSMR_HIP(hipMemsetAsync(dEnd.data(), 0, nRB * sizeof(u32), s));
-        if (pb > pa)
+        if (orig)
+            hipLaunchKernelGGL(k_rb_keys_csr, dim3(grid_for(M, 256)), dim3(256), 0, s, rowptr.data(),
+                               colidx.data(), M, RBr, N, keys.data(), vals.data(), qOf.data());
+        else if (pb > pa)
             hipLaunchKernelGGL(k_rb_keys, dim3(pb - pa), dim3(256), 0, s, sparseValueOffsets.data(),
                                sparseRel.data(), sparseColIdx.data(), pa, RBr, N, keys.data(),
                                vals.data(), qOf.data());
@@ -1037,10 +1102,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_HIP(hipGetLastError());
         BSMR_CHECK(sort_pairs64(keys.data(), skeys.data(), vals.data(), order.data(), n,
                                 bits_for(static_cast<u64>(nRB) * N), tmp, s));
-        hipLaunchKernelGGL(k_rb_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
-                           qOf.data(), sparseColIdx.data() + ebase, sparseValues.data() + ebase,
-                           dcol.data(), dout.data(), n0, n, RBr, L.meta.data(), L.out.data(),
-                           dEnd.data());
+        if (orig)  // vals = CSR positions: the output index is the entry itself
+            hipLaunchKernelGGL(k_rb_gather_csr, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
+                               qOf.data(), colidx.data(), n, RBr, L.meta.data(), L.out.data(),
+                               dEnd.data());
+        else
+            hipLaunchKernelGGL(k_rb_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
+                               qOf.data(), sparseColIdx.data() + ebase, sparseValues.data() + ebase,
+                               dcol.data(), dout.data(), n0, n, RBr, L.meta.data(), L.out.data(),
+                               dEnd.data());
         BSMR_HIP(hipGetLastError());
         BSMR_HIP(hipMemcpyAsync(rbEnd.data(), dEnd.data(), nRB * sizeof(u32), hipMemcpyDeviceToHost, s));
         BSMR_HIP(hipMemcpyAsync(hmeta.data(), L.meta.data(), n * sizeof(u32), hipMemcpyDeviceToHost, s));
@@ -1079,7 +1149,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         const u32 eb0 = b ? rbEnd[b - 1] : 0, eb1 = rbEnd[b];
         const u32 p0 = std::min(pa + b * (RBr / 16), pb), p1 = std::min(pa + (b + 1) * (RBr / 16), pb);
         // kept tiles of the row block: positions [t0, t0 + nt) of the kept list
-        const u32 t0 = keptPos[h_blockOffsets[p0] - T0], nt = keptPos[h_blockOffsets[p1] - T0] - t0;
+        const u32 t0 = orig ? 0 : keptPos[h_blockOffsets[p0] - T0];
+        const u32 nt = orig ? 0 : keptPos[h_blockOffsets[p1] - T0] - t0;
         u32 lo = eb0;
         for (u32 k = 0; k < NCR; ++k) {
             const size_t i = static_cast<size_t>(b) * NCR + k;
@@ -1250,6 +1321,12 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     L.pa = pa;
     L.pb = pb;
     L.rowEnd = qend;
+    if (orig) {
+        std::vector<u32> ids(M);
+        for (u32 r = 0; r < M; ++r) ids[r] = r;
+        BSMR_CHECK(L.rowIds.upload(ids.data(), std::max<u32>(M, 1), s));
+        BSMR_HIP(hipStreamSynchronize(s));
+    }
     L.tileMin = tileMin;
     L.nTilesKept = static_cast<u32>(hkept.size());
     L.nDemoted = nd;

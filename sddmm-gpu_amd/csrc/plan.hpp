@@ -114,11 +114,22 @@ struct Plan {
         // per row block: Σ over its items of (entries + pieces + 16 tiles + RB staged rows), the
         // shard cost model of bsmr_plan_shard
         std::vector<double> rbCost;
+        // original-order row blocks (banded / FEM patterns whose reordering scatters the band):
+        // row block b = original rows [b RB, (b + 1) RB), staged through rowIds (identity), every
+        // entry residual; whole-plan launches only (shards cut reordered panels)
+        bool orig = false;
+        DevBuf<u32> rowIds;
     };
     // rows of 128, 256, 512, 1024 and 2048 bytes, for fp32 [0, 5) and fp16/bf16 [5, 10) (tileMin)
     static constexpr int N_RB_SIZES = 5;
     static constexpr int N_RB_LAYOUTS = 2 * N_RB_SIZES;
     mutable RowBlockLayout rbl[N_RB_LAYOUTS];
+    // whole-plan original-order candidates (built for sparse-row patterns) and, per slot, whether
+    // the launch uses it: its column-run pieces are below 0.9 x the reordered layout's pieces +
+    // 16 per MFMA tile. BSMR_ORIG_ROWS: 0 = never, 1 = always, else auto
+    mutable RowBlockLayout rblo[N_RB_LAYOUTS];
+    mutable bool rb_use_orig[N_RB_LAYOUTS] = {};
+    int orig_rows = -1;
     // stored entries a dense tile needs to run on MFMA in the row-block launch (BSMR_TILE_MIN_F32
     // / BSMR_TILE_MIN_HALF); 0 = every tile. Measured (r01k sweep, profiles/r01k/tile_min.json):
     // fp32 MFMA (16x16x4) runs at the vector-FMA rate on gfx950 and a tile pays its empty slots,
@@ -128,7 +139,10 @@ struct Plan {
     // layouts of panel ranges (row-panel shards, bsmr_sddmm_panels), most recent last
     static constexpr size_t MAX_SHARD_LAYOUTS = 16;
     mutable std::vector<std::unique_ptr<RowBlockLayout>> shard_rbl;
-    int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin) const;
+    int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
+                              bool orig = false) const;
+    // the whole-plan layout a launch of this slot uses (rbl or rblo)
+    const RowBlockLayout& rb_whole(int slot) const { return rb_use_orig[slot] ? rblo[slot] : rbl[slot]; }
     // the (cached) layout for rows of rowBytes over panels [pa, pb) for fp32 (half = false) or
     // fp16/bf16 operands; null on error
     const RowBlockLayout* rowblock_layout(u32 rowBytes, bool half, u32 pa, u32 pb, int* err) const;

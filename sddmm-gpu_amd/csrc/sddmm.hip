@@ -887,9 +887,9 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.A = static_cast<const char*>(dA);
     a.B = static_cast<const char*>(dB);
     a.P = dP;
-    a.rows = p.rows.data();
+    a.rows = L.orig ? L.rowIds.data() : p.rows.data();
     a.R = L.rowEnd;
-    a.qbase = 16 * L.pa;
+    a.qbase = L.orig ? 0 : 16 * L.pa;
     a.N = p.N;
     a.RB = L.RB;
     a.items = L.items.data();

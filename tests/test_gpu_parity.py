@@ -228,6 +228,10 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     ({}, 32, 0),                               # 128-byte rows (8 rows per staged KiB)
     ({"BSMR_TILE_MIN_HALF": "0"}, 64, 1),      # 128-byte rows, half tiles on MFMA
     ({}, 64, 2),
+    ({"BSMR_ORIG_ROWS": "1"}, 128, 0),         # original-order row blocks, every entry residual
+    ({"BSMR_ORIG_ROWS": "1"}, 256, 1),
+    ({"BSMR_ORIG_ROWS": "1"}, 32, 0),
+    ({"BSMR_ORIG_ROWS": "1", "BSMR_L2_RANGE_KB": "64"}, 128, 0),
 ])
 def test_rowblock_layout_variants(monkeypatch, env, K, dtype):
     """Launch-layout switches (tile demotion thresholds, L2 column ranges, piece order) on the
@@ -284,3 +288,22 @@ def test_sddmm_batch_each_batch_checkdata(K, layout, nb):
     for b in range(nb):
         ref = O.sddmm_cpu(c, K, A[b * M * K:(b + 1) * M * K], B[b * N * K:(b + 1) * N * K])
         assert O.check_data(ref, P[b * nnz:(b + 1) * nnz]) == 0, b
+
+
+@pytest.mark.parametrize("K,dtype", [(128, 0), (256, 1), (64, 2)])
+def test_original_order_row_blocks_banded(K, dtype):
+    """Banded FEM-like pattern with random couplings (the C3 shape, small): the reordering
+    scatters the band, so the whole-plan launch picks original-order row blocks (sparse-row
+    rule, cost model); values match the oracle, and shards (reordered panel layouts) agree."""
+    M, N, rp, ci = synth.banded_fem_like(6000, 22, seed=5, band=48)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock")
+    A = make_data(M * K)
+    B = make_data(N * K)
+    P = run_sddmm(plan, A, B, K, len(ci), dtype=dtype)
+    if dtype:
+        A, B = half_values(A, dtype), half_values(B, dtype)
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
+    assert np.isfinite(P).all() and O.check_data(ref, P) == 0
+    shards = [plan.shard(K, r, 2, dtype) for r in range(2)]
+    Ps = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
+    assert np.isfinite(Ps).all() and O.check_data(ref, Ps) == 0
