@@ -1251,10 +1251,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         emit(spare, b, se0[i0], se1[i1] - se0[i0], st0[i0], st1[i1] - st0[i0], nu[b]);
     }
     {
-        for (size_t next = 0; next < lists[spare].size(); ++next) {
+        const size_t nsp = lists[spare].size();
+        for (size_t next = 0; next < nsp; ++next) {
             u32 x = 0;  // the list with the fewest items (ties: lowest index)
             for (u32 y = 1; y < XCD_BUCKETS; ++y)
                 if (lists[y].size() < lists[x].size()) x = y;
+            // original-order blocks (orig_contig): XCD x takes the x-th contiguous eighth, so the
+            // band's B rows of neighbouring blocks stay in one L2
+            if (orig && orig_contig && qSplit == 0)
+                x = static_cast<u32>(next * XCD_BUCKETS / nsp);
             lists[x].push_back(lists[spare][next]);
             lends[x].push_back(lends[spare][next]);
         }

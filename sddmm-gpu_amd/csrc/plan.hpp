@@ -130,6 +130,9 @@ struct Plan {
     mutable RowBlockLayout rblo[N_RB_LAYOUTS];
     mutable bool rb_use_orig[N_RB_LAYOUTS] = {};
     int orig_rows = -1;
+    // BSMR_ORIG_CONTIG: unsplit original-order blocks dealt as contiguous eighths per XCD (1)
+    // or to the shortest list (0); C3: 78.6 -> 76.8 us (profiles/r01s)
+    int orig_contig = 1;
     // stored entries a dense tile needs to run on MFMA in the row-block launch (BSMR_TILE_MIN_F32
     // / BSMR_TILE_MIN_HALF); 0 = every tile. Measured (r01k sweep, profiles/r01k/tile_min.json):
     // fp32 MFMA (16x16x4) runs at the vector-FMA rate on gfx950 and a tile pays its empty slots,
