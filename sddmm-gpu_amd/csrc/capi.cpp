@@ -75,6 +75,7 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     if (const char* orr = std::getenv("BSMR_ORIG_ROWS"))  // "0" never, "1" always, else auto
         p.orig_rows = orr[0] == '0' ? 0 : orr[0] == '1' ? 1 : -1;
     if (const char* oc = std::getenv("BSMR_ORIG_CONTIG")) p.orig_contig = std::atoi(oc);
+    if (const char* dk = std::getenv("BSMR_DENSE_KS")) p.dense_ks = std::atoi(dk);
     if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
         p.l2_range_kb = std::max(64, std::atoi(l2));
     u64 free_mem = o.free_mem_bytes;

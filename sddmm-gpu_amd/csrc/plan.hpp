@@ -169,6 +169,7 @@ struct Plan {
         DevBuf<u32> off, loc, out;  // loc = local row << 7 | local column; out = CSR position
     };
     mutable DenseLayout dense;
+    int dense_ks = 0;  // BSMR_DENSE_KS: 1 / 2 wave sets per tile, else by tile count
     int build_dense_layout() const;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);

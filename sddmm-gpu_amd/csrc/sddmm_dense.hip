@@ -63,13 +63,17 @@ __device__ __forceinline__ void lds_dma16(const char* g, char* l) {
                  : "memory", "m0");
 }
 
-// chunk kc of the tile's A and B rows into (sa, sb): KC/16 LDS-DMAs per wave and operand, no
-// branches (rows past M / N read the last row; they are never sampled)
-template <u32 KC>
+// LDS-DMAs per wave and operand for one chunk (16 KiB images of 1 KiB wave-instructions)
+template <u32 KC, u32 NWAV>
+constexpr u32 dense_nd() { return KC / 16 * 4 / NWAV; }
+
+// chunk kc of the tile's A and B rows into (sa, sb), spread over NWAV waves; no branches (rows
+// past M / N read the last row; they are never sampled)
+template <u32 KC, u32 NWAV>
 __device__ __forceinline__ void dense_stage(const DenseArgs& a, const u32 r0, const u32 c0,
                                             const u32 kc, const u32 ws, const u32 lane, char* sa,
                                             char* sb) {
-    constexpr u32 ND = KC / 16, GP = KC / 8;
+    constexpr u32 ND = dense_nd<KC, NWAV>(), GP = KC / 8;
     const size_t rowB = static_cast<size_t>(a.K) * 2;
 #pragma unroll
     for (u32 i = 0; i < ND; ++i) {
@@ -91,13 +95,16 @@ __device__ __forceinline__ f32x4 mfma16x16x32(const f32x4 x, const f32x4 y, cons
                                                        __builtin_bit_cast(b16x8, y), c, 0, 0, 0);
 }
 
-// one k-chunk of the wave's 64 x 64 quadrant from the images (sa, sb)
-template <int DT, u32 KC>
+// k-steps kset, kset + KS, ... of one k-chunk of the wave's 64 x 64 quadrant from the images
+// (sa, sb)
+template <int DT, u32 KC, u32 KS>
 __device__ __forceinline__ void dense_chunk(const char* sa, const char* sb, const u32 wy,
-                                            const u32 wx, const u32 lane, f32x4 (&acc)[4][4]) {
+                                            const u32 wx, const u32 lane, const u32 kset,
+                                            f32x4 (&acc)[4][4]) {
     const u32 rr = lane & 15, g4 = lane >> 4;
 #pragma unroll
-    for (u32 ks = 0; ks < KC / 32; ++ks) {
+    for (u32 k0 = 0; k0 < KC / 32; k0 += KS) {
+        const u32 ks = k0 + kset;
         f32x4 av[4], bv[4];
 #pragma unroll
         for (u32 i = 0; i < 4; ++i) {
@@ -118,9 +125,14 @@ constexpr u32 dense_lds() { return NS * 2 * chunk_bytes<KC>(); }
 template <u32 KC, u32 NS>
 constexpr u32 dense_wgs() { return 160u * 1024 / dense_lds<KC, NS>() < 4 ? 160u * 1024 / dense_lds<KC, NS>() : 4; }
 
-template <int DT, u32 KC, u32 NS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dense_wgs<KC, NS>())))
+// KS = 1: four waves, one 64 x 64 quadrant each. KS = 2: eight waves, waves 4..7 take the odd
+// k-steps of every chunk on the same quadrants (two waves per SIMD, so one wave's LDS reads run
+// under the other's MFMAs when the tiles give one workgroup per CU); partial tiles summed in LDS
+template <int DT, u32 KC, u32 NS, u32 KS>
+__global__ __launch_bounds__(256 * KS)
+__attribute__((amdgpu_waves_per_eu(dense_wgs<KC, NS>() * KS < 4 ? dense_wgs<KC, NS>() * KS : 4)))
 void k_sddmm_dense(DenseArgs a) {
+    constexpr u32 NT = 256 * KS, NWAV = 4 * KS, ND = dense_nd<KC, NWAV>();
     constexpr u32 CB = chunk_bytes<KC>(), LDS = dense_lds<KC, NS>();
     // NS stages of (A chunk, B chunk) images; the finished fp32 tile passes through the same
     // bytes, CR rows (of 512 bytes) at a time
@@ -141,7 +153,8 @@ void k_sddmm_dense(DenseArgs a) {
     const u32 tm = t / a.ntn, tn = t - tm * a.ntn;
     const u32 r0 = DT_TILE * tm, c0 = DT_TILE * tn;
     const u32 tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const u32 ws = __builtin_amdgcn_readfirstlane(w), wy = ws >> 1, wx = ws & 1;
+    const u32 ws = __builtin_amdgcn_readfirstlane(w), kset = ws >> 2, wy = (ws >> 1) & 1, wx = ws & 1;
+    static_assert(KS == 1 || (KS == 2 && KC / 32 == 2), "one k-step per wave set and chunk");
     f32x4 acc[4][4];
 #pragma unroll
     for (u32 i = 0; i < 4; ++i)
@@ -155,37 +168,45 @@ void k_sddmm_dense(DenseArgs a) {
     // branch around an LDS-DMA).
     auto stage = [&](const u32 kc) {
         char* const sa = st + (kc % NS) * (2 * CB);
-        dense_stage<KC>(a, r0, c0, min(kc, nk - 1), ws, lane, sa, sa + CB);
+        dense_stage<KC, NWAV>(a, r0, c0, min(kc, nk - 1), ws, lane, sa, sa + CB);
     };
 #pragma unroll
     for (u32 j = 0; j + 1 < NS; ++j) stage(j);
     for (u32 kc = 0; kc < nk; ++kc) {
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(KC / 8 * (NS - 2)) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * ND * (NS - 2)) : "memory");
         stage(kc + NS - 1);
         const char* const sa = st + (kc % NS) * (2 * CB);
-        dense_chunk<DT, KC>(sa, sa + CB, wy, wx, lane, acc);
+        dense_chunk<DT, KC, KS>(sa, sa + CB, wy, wx, lane, kset, acc);
     }
     // every read done, every LDS-DMA (the clamped tail prefetches too) landed: the images
     // become the fp32 tile
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     float* const ct = reinterpret_cast<float*>(st);
     // accumulator (i, jj) reg r of lane l = D[64 wy + 16 i + 4 (l >> 4) + r][64 wx + 16 jj + (l & 15)];
-    // pass h holds tile rows [CR h, CR h + CR)
+    // pass h holds tile rows [CR h, CR h + CR); KS = 2: wave set 1 stores its partial tile, set
+    // 0 adds its own
+    static_assert(KS == 1 || CR == DT_TILE, "split-k sums the whole tile in one pass");
 #pragma unroll
     for (u32 h = 0; h < DT_TILE / CR; ++h) {
         if (h) __syncthreads();  // the previous pass's reads are done
-        if (CR == DT_TILE || wy == h) {
 #pragma unroll
-            for (u32 i = 0; i < 4; ++i)
+        for (u32 set = KS; set-- > 0;) {
+            if (set == kset && (CR == DT_TILE || wy == h)) {
 #pragma unroll
-                for (u32 jj = 0; jj < 4; ++jj)
+                for (u32 i = 0; i < 4; ++i)
 #pragma unroll
-                    for (u32 r = 0; r < 4; ++r)
-                        ct[(64 * wy + 16 * i + 4 * (lane >> 4) + r - CR * h) * DT_TILE + 64 * wx +
-                           16 * jj + (lane & 15)] = acc[i][jj][r];
+                    for (u32 jj = 0; jj < 4; ++jj)
+#pragma unroll
+                        for (u32 r = 0; r < 4; ++r) {
+                            float& c = ct[(64 * wy + 16 * i + 4 * (lane >> 4) + r - CR * h) * DT_TILE +
+                                          64 * wx + 16 * jj + (lane & 15)];
+                            c = set + 1 < KS ? c + acc[i][jj][r] : acc[i][jj][r];
+                        }
+            }
+            if (set) __syncthreads();  // the later set's stores land before the earlier adds
         }
         __syncthreads();
-        for (u32 e = e0 + tid; e < e1; e += 256) {
+        for (u32 e = e0 + tid; e < e1; e += NT) {
             const u32 lc = a.loc[e] - CR * DT_TILE * h;  // loc = local row * 128 + local column
             if (lc < CR * DT_TILE) a.P[a.out[e]] = ct[lc];
         }
@@ -255,10 +276,18 @@ int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     // (KC, NS) = (64, 2): two workgroups per CU. Measured (tools/gpu_dense_stages.sh history,
     // r01q): 4 stages at one workgroup per CU and KC = 32 at 2-4 stages / 2-4 workgroups were
     // all slower (C5 uniform 10.6-12.1 us vs 8.8-9.8)
-    if (dtype == BSMR_F16)
-        hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2>), g, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2>), g, dim3(256), 0, s, a);
+    // split-k wave sets when the tiles fill at most one workgroup per CU (C5: 256 tiles)
+    const bool ks2 = p.dense_ks == 2 || (p.dense_ks != 1 && D.nonempty < 512);
+    if (ks2) {
+        if (dtype == BSMR_F16)
+            hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2, 2>), g, dim3(512), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2, 2>), g, dim3(512), 0, s, a);
+    } else if (dtype == BSMR_F16) {
+        hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2, 1>), g, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2, 1>), g, dim3(256), 0, s, a);
+    }
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }
