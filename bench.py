@@ -346,9 +346,10 @@ def main():
             "bytes_alg_per_launch": bytes_alg}
     dtiles = st_after.get("dense_sampled_tiles", 0)
     if dtiles:  # sddmm.hip use_dense: whole 128 x 128 tiles on the matrix cores
-        kern = (f"k_sddmm_dense<{'f16' if dtype == 1 else 'bf16'},64,2> (dense-sampled: {dtiles} "
-                "non-empty 128 x 128 MFMA tiles, K in 64-wide LDS-DMA chunks, stored entries "
-                "sampled from the fp32 tile)")
+        ks = 2 if dtiles < 512 else 1  # sddmm_dense.hip launch_dense (BSMR_DENSE_KS unset)
+        kern = (f"k_sddmm_dense<{'f16' if dtype == 1 else 'bf16'},64,2,{ks}> (dense-sampled: "
+                f"{dtiles} non-empty 128 x 128 MFMA tiles, {4 * ks} waves per tile, K in 64-wide "
+                "LDS-DMA chunks, stored entries sampled from the fp32 tile)")
         flops_tiles = 2.0 * dtiles * 128 * 128 * K
         ach = flops_tiles / (ms_per_step * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_HALF_PEAK_TFS,
