@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 #define BSMR_ABI_VERSION 4  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
-                              4: dense_sampled_tiles */
+                              4: dense_sampled_tiles, rb_orig_rows */
 
 typedef enum {
     BSMR_OK = 0,
@@ -131,6 +131,9 @@ typedef struct {
     /* fp16/bf16 dense-sampled launch (whole 128 x 128 MFMA tiles of P, patterns >= 5 % dense):
      * tiles holding at least one stored entry, 0 = not built */
     uint32_t dense_sampled_tiles;
+    /* bit i set: row-block layout i (as rb_rows) uses original-order row blocks (banded patterns
+     * whose reordering scatters the band) */
+    uint32_t rb_orig_rows;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

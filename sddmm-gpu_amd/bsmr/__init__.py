@@ -60,7 +60,7 @@ class PlanStats(C.Structure):
                 ("rb_rows", C.c_uint32 * 5), ("rb_items", C.c_uint32 * 5),
                 ("rb_pieces", C.c_uint32 * 5), ("rb_entries", C.c_uint32 * 5),
                 ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5),
-                ("dense_sampled_tiles", C.c_uint32)]
+                ("dense_sampled_tiles", C.c_uint32), ("rb_orig_rows", C.c_uint32)]
 
     def as_dict(self):
         d = {}

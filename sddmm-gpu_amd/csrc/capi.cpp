@@ -143,6 +143,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_entries[i] = L.rowBytes ? L.nEntries : 0;
         s->rb_tiles[i] = L.rowBytes ? L.nTilesKept : 0;
         s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
+        if (L.rowBytes && L.orig) s->rb_orig_rows |= 1u << i;
     }
     s->dense_sampled_tiles = p.dense.built ? p.dense.nonempty : 0;
     return BSMR_OK;

@@ -268,11 +268,16 @@ def test_values_independent_of_layout_permutation():
         assert O.check_data(ref, P) == 0
 
 
-@pytest.mark.parametrize("K,layout,nb", [(128, "auto", 3), (64, "colmajor", 2), (96, "auto", 4)])
-def test_sddmm_batch_each_batch_checkdata(K, layout, nb):
-    """sddmm_gpu_batch semantics: batch b = (A_b, B_b) at strides M*K / N*K, P_b at b*nnz."""
+@pytest.mark.parametrize("case,K,layout,nb", [("zipf", 128, "auto", 3), ("zipf", 64, "colmajor", 2),
+                                               ("zipf", 96, "auto", 4), ("banded", 128, "auto", 2)])
+def test_sddmm_batch_each_batch_checkdata(case, K, layout, nb):
+    """sddmm_gpu_batch semantics: batch b = (A_b, B_b) at strides M*K / N*K, P_b at b*nnz
+    (banded: the original-order row-block layout)."""
     torch = torch_cuda()
-    M, N, rp, ci = small_cases()["zipf"]
+    if case == "banded":
+        M, N, rp, ci = synth.banded_fem_like(3000, 22, seed=6, band=48)
+    else:
+        M, N, rp, ci = small_cases()[case]
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout=layout)
     A = make_data(nb * M * K)
     B = make_data(nb * N * K)[::-1].copy()  # different values per batch
@@ -290,8 +295,8 @@ def test_sddmm_batch_each_batch_checkdata(K, layout, nb):
         assert O.check_data(ref, P[b * nnz:(b + 1) * nnz]) == 0, b
 
 
-@pytest.mark.parametrize("K,dtype", [(128, 0), (256, 1), (64, 2)])
-def test_original_order_row_blocks_banded(K, dtype):
+@pytest.mark.parametrize("K,dtype,chosen", [(128, 0, True), (256, 1, True), (64, 2, None)])
+def test_original_order_row_blocks_banded(K, dtype, chosen):
     """Banded FEM-like pattern with random couplings (the C3 shape, small): the reordering
     scatters the band, so the whole-plan launch picks original-order row blocks (sparse-row
     rule, cost model); values match the oracle, and shards (reordered panel layouts) agree."""
@@ -304,6 +309,9 @@ def test_original_order_row_blocks_banded(K, dtype):
         A, B = half_values(A, dtype), half_values(B, dtype)
     ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
     assert np.isfinite(P).all() and O.check_data(ref, P) == 0
+    if chosen:  # (1024-row blocks of 128-byte rows: the rule may keep the reordered layout)
+        slot = {128: 0, 256: 1, 512: 2}[K * (4 if dtype == 0 else 2)]
+        assert plan.stats()["rb_orig_rows"] == 1 << slot  # the original-order layout was chosen
     shards = [plan.shard(K, r, 2, dtype) for r in range(2)]
     Ps = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
     assert np.isfinite(Ps).all() and O.check_data(ref, Ps) == 0
