@@ -577,7 +577,10 @@ __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const 
                                           f32x4 (&bv)[RowGeom<RBY>::NC]) {
     const u32 bb = col * RBY + 16 * sub;  // B < 4 GiB on this path (rb_slot)
 #pragma unroll
-    for (u32 f = 0; f < RowGeom<RBY>::NC; ++f) bv[f] = ld16(a.B + (bb + rot[f]));
+    for (u32 f = 0; f < RowGeom<RBY>::NC; ++f)
+        bv[f] = f + RowGeom<RBY>::RR <= RowGeom<RBY>::NC
+                    ? ld16(a.B + (bb + rot[0]) + 16 * RowGeom<RBY>::G * f)  // no wrap: immediate
+                    : ld16(a.B + (bb + rot[f]));
 }
 
 // a column-run piece of a row-group: entries [first, first + len), len <= RB_PIECE_MAX, all
