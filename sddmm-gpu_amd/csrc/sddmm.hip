@@ -646,9 +646,15 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
                     av[f] = h + f + RowGeom<RBY>::RR <= NC ? ld16(arot + 16 * G * (h + f))
                                                            : ld16(As + (ab + rot[h + f]));
 #pragma unroll
-                for (u32 f = 0; f < H; ++f) chunk_dot<DT>(av[f], bv[h + f], acc0, acc1);
+                for (u32 f = 0; f < H; ++f) {
+                    if constexpr (DT == 0)  // one packed chain: no acc0 + acc1 per entry
+                        chunk_dot<DT>(av[f], bv[h + f], acc0, acc0);
+                    else
+                        chunk_dot<DT>(av[f], bv[h + f], acc0, acc1);
+                }
             }
-            const f32x2 acc = acc0 + acc1;
+            f32x2 acc = acc0;
+            if constexpr (DT != 0) acc += acc1;
             float sm = acc.x + acc.y;
             sm += dppf<0xB1>(sm);                         // quad_perm [1,0,3,2]
             sm += dppf<0x4E>(sm);                         // quad_perm [2,3,0,1]
