@@ -620,6 +620,9 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
     for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
         if (G * k >= pc.len) break;
         const u32 nb = min(G, pc.len - G * k);
+        // fp32 images are unswizzled: broadcast the image row offset lr * RBY itself, computed
+        // once per batch by the lane that owns the entry, instead of shifting m in every step
+        const u32 mk = DT == 0 ? (pc.mm[k] >> 22) * RBY : pc.mm[k];
         float res = 0.f;
 #pragma unroll
         for (int i = 0; i < static_cast<int>(G); ++i) {
@@ -627,14 +630,19 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             u32 m;
             switch (i) {
 #define BSMR_C(I) \
-    case I: m = group_bcast<G, (I < G ? I : 0)>(pc.mm[k]); break;
+    case I: m = group_bcast<G, (I < G ? I : 0)>(mk); break;
                 BSMR_C(0) BSMR_C(1) BSMR_C(2) BSMR_C(3) BSMR_C(4) BSMR_C(5) BSMR_C(6) BSMR_C(7)
                 BSMR_C(8) BSMR_C(9) BSMR_C(10) BSMR_C(11) BSMR_C(12) BSMR_C(13) BSMR_C(14)
 #undef BSMR_C
-                default: m = group_bcast<G, G - 1>(pc.mm[k]); break;
+                default: m = group_bcast<G, G - 1>(mk); break;
             }
-            const u32 lr = m >> 22;
-            const u32 ab = lr * RBY + 16 * lds_chunk<DT>(lr, sub);  // + rot[f]: chunk G t + sub
+            u32 ab;  // + rot[f]: chunk G t + sub
+            if constexpr (DT == 0) {
+                ab = m + 16 * sub;
+            } else {
+                const u32 lr = m >> 22;
+                ab = lr * RBY + 16 * lds_chunk<DT>(lr, sub);
+            }
             const char* arot = As + (ab + rot[0]);                   // no wrap before f = NC - RR
             f32x2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
             constexpr u32 H = NC > 4 ? NC / 2 : NC;  // LDS reads in flight per half
