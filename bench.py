@@ -7,11 +7,17 @@ the plan of the C2 workload of BASELINE.json: nips-like 1,500 x 12,419 pattern w
 Reordering runs once before timing and is reported separately (the reference's GFLOP/s excludes it
 too, Logger.hpp:178-180). Inputs are resident in HBM when the timed region starts.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak scaling.
-Rank r owns row block r of an N-times taller pattern (each block the chosen workload's pattern),
-builds that block's plan and holds its A rows; B is generated on rank 0 and broadcast once over
-RCCL (xGMI) before timing. No collective in the data path; value = all ranks' flops / the slowest
-rank's time.
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): row-panel
+shards of ONE global BSMR plan (bsmr/dist.py). Rank 0 builds the plan and
+broadcasts its row stage (the clustering result) over RCCL; every rank rebuilds the column stage
+from it, cuts the same contiguous panel ranges, uploads only its panels' A rows and runs
+bsmr_sddmm_panels_local; B is broadcast once from rank 0 over RCCL (xGMI); after timing P is
+sum-reduced to rank 0 and checked against the product's host SDDMM (checkData rule).
+  * C2 (default): weak scaling. The global pattern is N copies of the nips-like pattern stacked
+    vertically, copy b with its columns relabelled by a random permutation (synth.stack_copies),
+    so per-GPU work stays one C2 while the plan, the cut and the split are real.
+  * C3/C4/C5: strong scaling of the one matrix (C4: the north_star reddit split).
+No collective in the timed loop; value = all ranks' flops / the slowest rank's time.
 
 Other BASELINE.json configs (extra measurements, not the driver's line): --config C3 (cop20k-like,
 fp16, K=256), C4 (reddit-like power-law graph, fp32, K=128; --scale shrinks it), C5 (DLMC-like
@@ -158,11 +164,8 @@ def vendor_baseline(M, N, K, rp, ci, dA, dB, P_engine, dtype, stream, flops, eng
     import numpy as np
     import torch
 
-    from bsmr import BsmrError
+    from bsmr import BsmrError, check_data
     from bsmr.vendor import RocsparseSddmm
-
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
 
     dev = dA.device
     d_rp = torch.from_numpy(rp.astype(np.int32)).to(dev)
@@ -205,7 +208,7 @@ def vendor_baseline(M, N, K, rp, ci, dA, dB, P_engine, dtype, stream, flops, eng
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / iters
         r = {"value": round(flops / (ms * 1e-3) / 1e9, 2), "ms": round(ms, 5), "iters": iters,
-             "checkData_errors_vs_engine": O.check_data(dP.cpu().numpy(), P_engine)}
+             "checkData_errors_vs_engine": check_data(dP.cpu().numpy(), P_engine)}
         out[alg] = r
         del rs, dP
         if r["checkData_errors_vs_engine"] == 0 and (best is None or ms < best[1]):
@@ -216,24 +219,72 @@ def vendor_baseline(M, N, K, rp, ci, dA, dB, P_engine, dtype, stream, flops, eng
     return out
 
 
+def kernel_name(st, st_after, K, dtype, layout):
+    """The launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half / use_dense)."""
+    from bsmr import F32
+
+    rby = K * (4 if dtype == F32 else 2)
+    tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
+    if rby in (128, 256, 512, 1024, 2048) and layout != "colmajor" and not tile_dominated:
+        tiles = ("fp32 tiles demoted to residual entries" if dtype == F32
+                 else "dense-tile MFMA for tiles >= 128 entries")
+        rows = st_after["rb_rows"][{128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]]
+        nt = 1024 if rby * rows > 80 * 1024 else 512
+        return (f"k_sddmm_rb<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
+                f"rows per block: residual entries; {tiles})"), rby
+    if dtype == F32:
+        return f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)", rby
+    return f"k_sddmm_half<{'f16' if dtype == 1 else 'bf16'}> (dense-tile MFMA + residual)", rby
+
+
+def traffic_for(args, K):
+    """roofline.traffic: HBM bytes per launch from the committed PMC summary of this config
+    (tools/pmc_traffic.py), only if it was measured on the kernel sources of this tree (their
+    sha256 is recorded in the file); None otherwise."""
+    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}_K{K}.json")
+    if not os.path.exists(tj):
+        return None, None
+    with open(tj) as f:
+        t = json.load(f)
+    import hashlib
+
+    srcs = t.get("kernel_sources_sha256")
+    if not srcs:
+        return None, {"file": os.path.relpath(tj, ROOT), "status": "no source hash: not used"}
+    for rel, h in srcs.items():
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            if hashlib.sha256(f.read()).hexdigest() != h:
+                return None, {"file": os.path.relpath(tj, ROOT),
+                              "status": f"stale: {rel} changed since the PMC run"}
+    return t.get("hbm_bytes_per_launch"), {"file": os.path.relpath(tj, ROOT),
+                                           "measured_on": t.get("measured_on"),
+                                           "status": "kernel sources match"}
+
+
 def main():
     args = parse()
-    import numpy as np
     import torch
 
-    from bsmr import F32, Plan, make_data
     from bsmr import dist as D
 
     rank, world, local = D.env_rank_world()
-    dist = None
     if world > 1:
-        import torch.distributed as dist  # noqa: F811
         # one rank per GPU; BSMR_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
         # multi-process path (ranks then share devices; their timings are not a measurement)
         torch.cuda.set_device(local % torch.cuda.device_count())
         D.init(os.environ.get("BSMR_DIST_BACKEND", "nccl"))  # nccl = RCCL over xGMI
-    else:
-        torch.cuda.set_device(0)
+        return main_sharded(args, rank, world)
+    torch.cuda.set_device(0)
+    return main_single(args)
+
+
+def main_single(args):
+    import numpy as np  # noqa: F401
+    import torch
+
+    from bsmr import F32, Plan, make_data
+
+    world = 1
     dev = torch.device("cuda", torch.cuda.current_device())
 
     (M, N, rp, ci), K, dtype, desc = workload(args)
@@ -245,21 +296,10 @@ def main():
     st = plan.stats()
 
     tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
-    A = make_data(M * K)  # this rank's A rows (Matrix<float>(M,K,row_major).makeData)
+    A = make_data(M * K)  # Matrix<float>(M,K,row_major).makeData
     dA = torch.from_numpy(A).to(dev).to(tdt)
-    if rank == 0:
-        B = make_data(N * K)
-        dB = torch.from_numpy(B).to(dev).to(tdt)
-    else:
-        B = None
-        dB = torch.empty(N * K, dtype=tdt, device=dev)
-    bcast_ms = 0.0
-    if dist is not None:
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        D.broadcast_(dB, 0)  # B broadcast once over RCCL/xGMI
-        torch.cuda.synchronize()
-        bcast_ms = (time.perf_counter() - tb) * 1e3
+    B = make_data(N * K)  # Matrix<float>(K,N,col_major).makeData
+    dB = torch.from_numpy(B).to(dev).to(tdt)
     dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
@@ -269,21 +309,15 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if dist is not None:
-        dist.barrier()
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
+    e0.record(stream)  # HIP events on the launch stream
     for _ in range(args.steps):
         step()
     e1.record(stream)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
     ms = e0.elapsed_time(e1)
-    if dist is not None:
-        ms = D.max_over_ranks(ms, dev)  # whole-job time = slowest rank
     ms_per_step = ms / args.steps
 
     # cold: before each step a 512 MiB write evicts the Infinity Cache (MALL) and the L2s, so
@@ -303,8 +337,6 @@ def main():
         torch.cuda.synchronize()
         cold_ms = statistics.median(a.elapsed_time(b) for a, b in evs)
         del junk
-        if dist is not None:
-            cold_ms = D.max_over_ranks(cold_ms, dev)
 
     # the same kernel split into its dense-tile-only and residual-only launches
     prof = {} if args.no_split else plan.profile(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
@@ -317,33 +349,14 @@ def main():
     value = flops_rank * world / (ms_per_step * 1e-3) / 1e9
     bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
     achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
-    traffic = None
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}_K{K}.json")
-    if os.path.exists(tj):
-        with open(tj) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic, traffic_src = traffic_for(args, K)
 
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-    # the launch bsmr_sddmm picks (sddmm.hip rb_slot / launch_half)
-    rby = K * (4 if dtype == F32 else 2)
-    tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
-    if rby in (128, 256, 512, 1024, 2048) and args.layout != "colmajor" and not tile_dominated:
-        tiles = ("fp32 tiles demoted to residual entries" if dtype == F32
-                 else "dense-tile MFMA for tiles >= 128 entries")
-        rows = st_after["rb_rows"][{128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]]
-        nt = 1024 if rby * rows > 80 * 1024 else 512
-        kern = (f"k_sddmm_rb<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
-                f"rows per block: residual entries; {tiles})")
-    elif dtype == F32:
-        kern = f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)"
-    else:
-        kern = f"k_sddmm_half<{'f16' if dtype == 1 else 'bf16'}> (dense-tile MFMA + residual)"
+    kern, rby = kernel_name(st, st_after, K, dtype, args.layout)
+    no_tiles = (kern.startswith("k_sddmm_rb") and
+                not st_after["rb_tiles"][{128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]])
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kern,
-            "bytes_alg_per_launch": bytes_alg}
+            "bytes_alg_per_launch": bytes_alg, "traffic_source": traffic_src}
     dtiles = st_after.get("dense_sampled_tiles", 0)
     if dtiles:  # sddmm.hip use_dense: whole 128 x 128 tiles on the matrix cores
         ks = 2 if dtiles < 512 else 1  # sddmm_dense.hip launch_dense (BSMR_DENSE_KS unset)
@@ -355,6 +368,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_HALF_PEAK_TFS,
                 "unit": "TFLOP/s", "frac": round(ach / MFMA_HALF_PEAK_TFS, 4), "traffic": traffic,
                 "kernel": kern, "flops_alg_per_launch": flops_tiles,
+                "traffic_source": traffic_src,
                 "hbm_bytes_alg_per_launch": bytes_alg,
                 "note": "algorithmic FLOPs of the tiles computed (the dense-sampled launch "
                         "computes every product of a non-empty tile)"}
@@ -372,18 +386,20 @@ def main():
         "dtype": {0: "f32", 1: "f16", 2: "bf16"}[dtype],
         "data": "synthetic",
         "config": {
-            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}, "
-                               "one plan per rank (row block)",
+            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}",
             "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
-            "parallelism": f"row-panel blocks x{world}, B broadcast (RCCL)",
+            "parallelism": "single GPU, whole plan (one launch per step)",
             "num_clusters": st["num_clusters"], "dense_tiles": st["num_dense_tiles"],
             "residual_nnz": st["num_residual"],
             "plan_build_s": round(plan_s, 3), "row_reorder_ms": round(st["row_reorder_ms"], 3),
-            "col_reorder_ms": round(st["col_reorder_ms"], 3), "b_broadcast_ms": round(bcast_ms, 3),
+            "col_reorder_ms": round(st["col_reorder_ms"], 3),
             "rowblock_layout": {k: st_after[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
         },
         "roofline": roof,
-        "kernels_ms": {k: round(v, 5) for k, v in prof.items()},
+        # the launch's dense-tile-only / residual-only halves (None when the layout keeps no
+        # MFMA tiles: fp32 row-block plans demote every tile)
+        "kernels_ms": {k: (None if k == "dense_ms" and no_tiles else round(v, 5))
+                       for k, v in prof.items()},
     }
     if kern.startswith("k_sddmm_rb"):
         out["bounds"] = rowblock_bounds(st_after, rby, ms_per_step)
@@ -391,7 +407,7 @@ def main():
         out["cold"] = {"ms_per_step": round(cold_ms, 5),
                        "value": round(flops_rank * world / (cold_ms * 1e-3) / 1e9, 2),
                        "note": "median of steps each preceded by a 512 MiB write (MALL evicted)"}
-    if not args.no_vendor and world == 1:
+    if not args.no_vendor:
         out["vendor_baseline"] = vendor_baseline(M, N, K, rp, ci, dA, dB, P_gpu, dtype, stream,
                                                  flops_rank, ms_per_step)
     if not args.no_cpu_baseline:
@@ -402,8 +418,165 @@ def main():
             Br = dB.float().cpu().numpy()
         out["cpu_baseline"] = cpu_baseline(M, N, rp, ci, K, Ar, Br, P_gpu)
     print(json.dumps(out), flush=True)
-    if dist is not None:
+
+
+def sharded_workload(args, world):
+    """(pattern, K, dtype, description, scaling) of a multi-GPU run: C2 weak (world stacked
+    copies of the nips-like pattern), the other configs strong (one matrix split)."""
+    from bsmr import synth
+
+    (M, N, rp, ci), K, dtype, desc = workload(args)
+    if args.config != "C2":
+        return (M, N, rp, ci), K, dtype, desc, "strong"
+    return (synth.stack_copies(M, N, rp, ci, world), K, dtype,
+            desc + f"; x{world} stacked copies (copy b: columns relabelled by a random "
+                   "permutation, synth.stack_copies), one C2 per GPU", "weak")
+
+
+def main_sharded(args, rank, world):
+    """Row-panel shards of one global plan over `world` ranks (bsmr/dist.py)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from bsmr import F32, check_data, make_data, sddmm_cpu
+    from bsmr import dist as D
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    (M, N, rp, ci), K, dtype, desc, scaling = sharded_workload(args, world)
+    nnz = len(ci)
+    plan, pinfo = D.distribute_plan(M, N, rp, ci, dev, alpha=args.alpha, delta=args.delta,
+                                    layout=args.layout)
+    st = plan.stats()
+    t0 = time.perf_counter()
+    p0, p1 = plan.shard(K, rank, world, dtype)  # same cuts on every rank (same global plan)
+    cut_s = time.perf_counter() - t0
+    rows = plan.array("reorderedRows")
+
+    tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
+    # A partitioned: the makeData stream is a function of the row, so every rank derives its own
+    # panels' rows locally (nothing of A is sent); only they reach this GPU
+    A = make_data(M * K)
+    A_local = D.shard_a_rows(A, K, rows, p0, p1)
+    dA = torch.from_numpy(A_local.reshape(-1)).to(dev).to(tdt)
+    if dA.numel() == 0:
+        dA = torch.zeros(K, dtype=tdt, device=dev)
+    # B broadcast once from rank 0 over RCCL (xGMI)
+    if rank == 0:
+        B = make_data(N * K)
+        dB = torch.from_numpy(B).to(dev).to(tdt)
+    else:
+        B = None
+        dB = torch.empty(N * K, dtype=tdt, device=dev)
+    dist.barrier()
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
+    D.broadcast_(dB, 0)
+    torch.cuda.synchronize()
+    bcast_ms = (time.perf_counter() - tb) * 1e3
+    dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        plan.sddmm_panels_local(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), p0, p1,
+                                stream=sp, dtype=dtype)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    ms_mine = e0.elapsed_time(e1) / args.steps
+    ms_all = D.all_values(ms_mine, dev)
+    ms_per_step = max(ms_all)  # whole-job time = slowest rank
+
+    # this rank's share: stored entries of its panels
+    lens = np.diff(rp.astype(np.int64))
+    mine = int(lens[rows[16 * p0:min(16 * p1, len(rows))]].sum())
+    entries_all = D.all_values(mine, dev)
+    panels_all = D.all_values(p1 - p0, dev)
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    P = D.gather_p(dP, 0)  # sum-reduce: each output written by exactly one rank
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    st_after = plan.stats()
+    if rank != 0:
         dist.destroy_process_group()
+        return
+    # checkData of the assembled P against the product's host SDDMM (host.cpp:45-76)
+    if dtype == F32:
+        Ar, Br = A, B
+    else:
+        Ar = torch.from_numpy(A).to(tdt).float().numpy()
+        Br = dB.float().cpu().numpy()
+    ref = sddmm_cpu(M, N, rp, ci, K, Ar, Br,
+                    threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    nerr = check_data(ref, P)
+
+    flops = 2.0 * nnz * K
+    value = flops / (ms_per_step * 1e-3) / 1e9
+    s = 4 if dtype == F32 else 2
+    bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
+    achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
+    kern, _ = kernel_name(st, st_after, K, dtype, args.layout)
+    mean_ms = sum(ms_all) / world
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": {0: "f32", 1: "f16", 2: "bf16"}[dtype],
+        "data": "synthetic",
+        "config": {
+            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}",
+            "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
+            "parallelism": (f"row-panel shards x{world} of one global BSMR plan (rank 0 clusters, "
+                            "row stage broadcast over RCCL, column stage rebuilt per rank), A "
+                            "rows local to their shard, B broadcast once (RCCL), P sum-reduced "
+                            "to rank 0"),
+            "backend": dist.get_backend(),
+            "num_clusters": st["num_clusters"], "num_row_panels": st["num_row_panels"],
+            "plan_build_s": round(pinfo["plan_build_s"], 3),
+            "row_reorder_ms": round(st["row_reorder_ms"], 3),
+            "plan_distribution_ms": round(pinfo["distribute_ms"], 3),
+            "row_stage_bcast_ms": round(pinfo["row_stage_bcast_ms"], 3),
+            "row_stage_bytes": pinfo["row_stage_bytes"],
+            "shard_cut_s": round(cut_s, 3),
+            "b_broadcast_ms": round(bcast_ms, 3),
+            "p_gather_ms": round(gather_ms, 3),
+        },
+        "shards": {
+            "panels": [int(x) for x in panels_all],
+            "entries": [int(x) for x in entries_all],
+            "ms_per_step": [round(x, 5) for x in ms_all],
+            "imbalance_max_over_mean": round(ms_per_step / mean_ms, 3),
+            "kernel": "bsmr_sddmm_panels_local -> " + kern,
+        },
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                     "frac": round(achieved / (HBM_PEAK_GBS * world), 4), "traffic": None,
+                     "kernel": kern, "bytes_alg_per_launch": bytes_alg,
+                     "note": "whole-job algorithmic bytes per step over the slowest rank's time, "
+                             "against world x 8 TB/s"},
+        "checkData_errors_gathered_P": nerr,
+    }
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -22,8 +22,9 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 4  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
-                              4: dense_sampled_tiles, rb_orig_rows */
+#define BSMR_ABI_VERSION 5  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+                              4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
+                              bsmr_sddmm_panels_local, host SDDMM + checkData */
 
 typedef enum {
     BSMR_OK = 0,
@@ -100,6 +101,32 @@ void bsmr_plan_options_default(bsmr_plan_options* o);
  * GPU. Host CSR in, device-resident plan out. */
 int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M, uint32_t N,
                      uint32_t nnz, const bsmr_plan_options* opt, bsmr_plan** out);
+/* Row stage of a plan (BSMR::rowReordering, BSMR.cpp:27-50 / rowReordering.cu:1027-1095): the
+ * clustering result that multi-GPU runs compute once and broadcast (a bit-exact
+ * permutation needs the global first-fit over all rows). */
+typedef struct {
+    uint32_t M, N, nnz;
+    uint32_t block_size, num_blocks_per_row, cluster_block_dim;
+    uint32_t num_zero_rows;        /* rows dropped before the panels (rowReordering.cu:1081-1090) */
+    uint32_t num_reordered_rows;   /* R = M - num_zero_rows: length of the rows array */
+    int32_t num_clusters;          /* bsmr_numClusters */
+    float alpha;                   /* the similarity threshold the rows were clustered with */
+    float row_reorder_ms;
+    uint64_t exact_similarity_evals, total_similarity_evals;
+} bsmr_row_stage;
+
+/* Copy the row stage out: hdr always, the reordered rows (num_reordered_rows uint32) into `rows`
+ * when non-NULL; `rows` may be host or device memory (e.g. the buffer a broadcast sends). */
+int bsmr_plan_export_rows(const bsmr_plan* plan, bsmr_row_stage* hdr, uint32_t* rows);
+/* Build a plan from an exported row stage without clustering again: the same CSR, the header and
+ * rows (host or device memory; checked to be the non-empty rows of S, each once), then the
+ * column reordering and tile layout for opt->delta (alpha is the header's). The result is
+ * identical to bsmr_plan_create's plan for (alpha, delta); parity arrays DISPERSION/ASCENDING
+ * are not kept (length 0). */
+int bsmr_plan_import_rows(const uint32_t* rowptr, const uint32_t* colidx,
+                          const bsmr_row_stage* hdr, const uint32_t* rows,
+                          const bsmr_plan_options* opt, bsmr_plan** out);
+
 /* Test-mode split (sddmm.cu:62-118): keep the row reordering, redo the column split for delta. */
 int bsmr_plan_recolumn(bsmr_plan* plan, float delta);
 void bsmr_plan_destroy(bsmr_plan* plan);
@@ -200,12 +227,34 @@ int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* sparseValueOff
 int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
                       int dtype, float* dP, uint32_t p0, uint32_t p1, void* stream);
 
+/* The same shard launch with a shard-local A: dA_local holds only the A rows of reordered
+ * positions [16 p0, min(16 p1, R)) in that order (row j = A row reorderedRows[16 p0 + j]), so a
+ * rank receives just its panels' rows ("A partitioned"). dB and dP as in
+ * bsmr_sddmm (whole B, P in CSR order; only the shard's outputs are written). Row-block launches
+ * only (rows of 128 B .. 2 KiB), else BSMR_ERR_UNSUPPORTED. */
+int bsmr_sddmm_panels_local(const bsmr_plan* plan, const void* dA_local, const void* dB,
+                            uint32_t K, int dtype, float* dP, uint32_t p0, uint32_t p1,
+                            void* stream);
+
 /* Timing: run `iters` back-to-back SDDMMs on `stream`, timing each kernel with HIP events on
  * that stream. Outputs average ms per launch of the dense-tile kernel, the residual kernel and
  * the whole SDDMM. */
 int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
                        int dtype, float* dP, int iters, void* stream, float* ms_dense,
                        float* ms_residual, float* ms_total);
+
+/* ------------------------------------------------------------------- validation ---- */
+/* Replaces sddmm_cpu(A, B, S, P) (src/host.cpp:45-76): host SDDMM in the reference's loop order
+ * (per stored entry a serial fp32 `val += A[r*K+k] * B[c*K+k]`, k ascending, no FMA), rows split
+ * over nthreads host threads (0 = all cores); P receives nnz values in CSR order. */
+int bsmr_sddmm_cpu(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M, uint32_t N,
+                   uint32_t K, const float* A, const float* B, float* P, int nthreads);
+/* Replaces checkOneData<float> (include/checkData.hpp:21-30): 1 if |a-b| < 1e-5 or
+ * |a-b| / max(|a|, |b|, 1e-3) < 1e-3. */
+int bsmr_check_one(float data1, float data2);
+/* Replaces checkDataFunction (include/checkData.hpp:44-79): returns the number of mismatches;
+ * verbose != 0 prints the reference's framed report (first 9 errors, error rate) on stdout. */
+uint64_t bsmr_check_data(uint64_t n, const float* data1, const float* data2, int verbose);
 
 #ifdef __cplusplus
 }

@@ -79,7 +79,28 @@ class EvalStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-ABI_VERSION = 4  # include/bsmr.h BSMR_ABI_VERSION
+class RowStage(C.Structure):
+    """bsmr_row_stage: the clustering result a multi-GPU run computes once and broadcasts."""
+    _fields_ = [("M", C.c_uint32), ("N", C.c_uint32), ("nnz", C.c_uint32),
+                ("block_size", C.c_uint32), ("num_blocks_per_row", C.c_uint32),
+                ("cluster_block_dim", C.c_uint32), ("num_zero_rows", C.c_uint32),
+                ("num_reordered_rows", C.c_uint32), ("num_clusters", C.c_int32),
+                ("alpha", C.c_float), ("row_reorder_ms", C.c_float),
+                ("exact_similarity_evals", C.c_uint64), ("total_similarity_evals", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+    def to_array(self):
+        """The header as bytes in a uint8 array (to ship it in a broadcast)."""
+        return np.frombuffer(bytes(self), dtype=np.uint8).copy()
+
+    @classmethod
+    def from_array(cls, a):
+        return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
+
+
+ABI_VERSION = 5  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -89,8 +110,9 @@ EXPORTS = [
     "bsmr_make_data", "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
     "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
     "bsmr_sddmm", "bsmr_sddmm_batch", "bsmr_plan_shard", "bsmr_plan_shard_dtype",
-    "bsmr_shard_cuts", "bsmr_sddmm_panels",
-    "bsmr_sddmm_profile",
+    "bsmr_shard_cuts", "bsmr_sddmm_panels", "bsmr_sddmm_panels_local",
+    "bsmr_plan_export_rows", "bsmr_plan_import_rows",
+    "bsmr_sddmm_profile", "bsmr_sddmm_cpu", "bsmr_check_one", "bsmr_check_data",
 ]
 
 _lib = None
@@ -147,6 +169,17 @@ def lib():
     L.bsmr_shard_cuts.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_int, _u32p]
     L.bsmr_sddmm_panels.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
                                     C.c_uint32, vp]
+    L.bsmr_sddmm_panels_local.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
+                                          C.c_uint32, vp]
+    L.bsmr_plan_export_rows.argtypes = [vp, C.POINTER(RowStage), vp]
+    L.bsmr_plan_import_rows.argtypes = [_u32p, _u32p, C.POINTER(RowStage), vp,
+                                        C.POINTER(PlanOptions), C.POINTER(vp)]
+    L.bsmr_sddmm_cpu.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_uint32, _f32p, _f32p,
+                                 _f32p, C.c_int]
+    L.bsmr_check_one.restype = C.c_int
+    L.bsmr_check_one.argtypes = [C.c_float, C.c_float]
+    L.bsmr_check_data.restype = C.c_uint64
+    L.bsmr_check_data.argtypes = [C.c_uint64, _f32p, _f32p, C.c_int]
     L.bsmr_sddmm_profile.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_int, vp,
                                      C.POINTER(C.c_float), C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]
@@ -232,7 +265,8 @@ class Plan:
     """Device-resident BSMR plan (reordered rows, dense 16x16 tiles, residual lists)."""
 
     def __init__(self, M, N, rowptr, colidx, alpha=0.3, delta=0.3, free_mem_bytes=0, device=0,
-                 cluster_batch=0, exact_similarity=False, layout="auto", lds_budget_kb=0):
+                 cluster_batch=0, exact_similarity=False, layout="auto", lds_budget_kb=0,
+                 _row_stage=None):
         rowptr = np.ascontiguousarray(rowptr, np.uint32)
         colidx = np.ascontiguousarray(colidx, np.uint32)
         o = PlanOptions()
@@ -247,9 +281,41 @@ class Plan:
         o.lds_budget_kb = int(lds_budget_kb)
         self.M, self.N, self.nnz = int(M), int(N), int(len(colidx))
         h = C.c_void_p()
-        _check(lib().bsmr_plan_create(rowptr, colidx, M, N, len(colidx), C.byref(o), C.byref(h)),
-               "bsmr_plan_create")
+        if _row_stage is None:
+            _check(lib().bsmr_plan_create(rowptr, colidx, M, N, len(colidx), C.byref(o),
+                                          C.byref(h)), "bsmr_plan_create")
+        else:
+            hdr, rows_ptr = _row_stage
+            _check(lib().bsmr_plan_import_rows(rowptr, colidx, C.byref(hdr), rows_ptr,
+                                               C.byref(o), C.byref(h)), "bsmr_plan_import_rows")
         self.h = h
+
+    @classmethod
+    def from_row_stage(cls, rowptr, colidx, hdr, rows, delta=0.3, device=0, layout="auto",
+                       lds_budget_kb=0):
+        """bsmr_plan_import_rows: the plan of an exported row stage (no clustering). rows: a
+        uint32 numpy array, or an int device pointer (e.g. a broadcast tensor's data_ptr())."""
+        if isinstance(rows, np.ndarray):
+            rows = np.ascontiguousarray(rows, np.uint32)
+            ptr = rows.ctypes.data
+        else:
+            ptr = int(rows)
+        return cls(hdr.M, hdr.N, rowptr, colidx, alpha=hdr.alpha, delta=delta, device=device,
+                   layout=layout, lds_budget_kb=lds_budget_kb, _row_stage=(hdr, ptr))
+
+    def export_rows(self, rows_out=None):
+        """bsmr_plan_export_rows: (header, rows). rows_out: None (a numpy array is returned) or
+        an int pointer (host or device) receiving num_reordered_rows uint32."""
+        hdr = RowStage()
+        _check(lib().bsmr_plan_export_rows(self.h, C.byref(hdr), None), "bsmr_plan_export_rows")
+        if rows_out is None:
+            rows = np.empty(max(hdr.num_reordered_rows, 1), np.uint32)
+            _check(lib().bsmr_plan_export_rows(self.h, C.byref(hdr), rows.ctypes.data),
+                   "bsmr_plan_export_rows")
+            return hdr, rows[:hdr.num_reordered_rows]
+        _check(lib().bsmr_plan_export_rows(self.h, C.byref(hdr), int(rows_out)),
+               "bsmr_plan_export_rows")
+        return hdr, None
 
     def recolumn(self, delta):
         _check(lib().bsmr_plan_recolumn(self.h, float(np.float32(delta))), "bsmr_plan_recolumn")
@@ -287,6 +353,11 @@ class Plan:
         _check(lib().bsmr_sddmm_panels(self.h, dA, dB, K, dtype, dP, p0, p1, stream or None),
                "bsmr_sddmm_panels")
 
+    def sddmm_panels_local(self, dA_local, dB, K, dP, p0, p1, stream=0, dtype=F32):
+        """Shard launch with a shard-local A: rows of reordered positions [16 p0, 16 p1)."""
+        _check(lib().bsmr_sddmm_panels_local(self.h, dA_local, dB, K, dtype, dP, p0, p1,
+                                             stream or None), "bsmr_sddmm_panels_local")
+
     def shard(self, K, rank, world, dtype=F32):
         """Panel range [p0, p1) of `rank` (bsmr_plan_shard_dtype)."""
         p0, p1 = C.c_uint32(), C.c_uint32()
@@ -315,3 +386,22 @@ def shard_cuts(block_offsets, sparse_value_offsets, K, world):
     cuts = np.zeros(world + 1, np.uint32)
     _check(lib().bsmr_shard_cuts(bo, so, P, K, world, cuts), "bsmr_shard_cuts")
     return cuts
+
+
+def sddmm_cpu(M, N, rowptr, colidx, K, A, B, threads=0):
+    """bsmr_sddmm_cpu: the reference's host SDDMM (host.cpp:45-76) as product code."""
+    rowptr = np.ascontiguousarray(rowptr, np.uint32)
+    colidx = np.ascontiguousarray(colidx, np.uint32)
+    P = np.empty(len(colidx), np.float32)
+    _check(lib().bsmr_sddmm_cpu(rowptr, colidx, M, N, K, np.ascontiguousarray(A, np.float32),
+                                np.ascontiguousarray(B, np.float32), P, threads), "bsmr_sddmm_cpu")
+    return P
+
+
+def check_data(data1, data2, verbose=False):
+    """bsmr_check_data (checkData.hpp:44-79): number of mismatches; verbose prints the report."""
+    a = np.ascontiguousarray(data1, np.float32)
+    b = np.ascontiguousarray(data2, np.float32)
+    if a.shape != b.shape:
+        raise ValueError("check_data: sizes differ")
+    return int(lib().bsmr_check_data(a.size, a, b, 1 if verbose else 0))

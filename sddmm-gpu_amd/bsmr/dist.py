@@ -1,11 +1,28 @@
-"""Multi-GPU plumbing for row-panel sharded runs: one process per GPU over
-torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" for CPU tests).
+"""Row-panel sharded SDDMM over several GPUs: one process per GPU over
+torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" for CPU tests and 1-GPU
+rehearsals).
 
-The SDDMM data path has no collective: every rank computes the outputs of its own row panels.
-The only exchanges are setup (B broadcast once from rank 0) and reporting (the slowest rank's
-time, per-rank counts).
+The reference has no multi-GPU code (its launcher is single-GPU, sddmmKernel.cu:2540-2663). The
+split built here:
+
+1. **Global plan, clustered once.** A bit-exact permutation needs the global first-fit over all
+   rows, so rank 0 builds the plan (``bsmr_plan_create``) and broadcasts its row stage (the
+   ``bsmr_row_stage`` header and the reordered rows, u32 on the device) over RCCL. The other
+   ranks rebuild the column stage from it (``bsmr_plan_import_rows``): clustering is >99 % of the
+   plan time (reddit_like x1: 85.8 s of 86 s), the column stage a deterministic O(nnz) pass
+   (0.14 s) that is cheaper to recompute than to ship (its arrays are ~12 B per entry).
+2. **Panel cut.** Every rank holds the same global plan, so every rank computes the same cost-model
+   cuts (``bsmr_plan_shard_dtype``) without talking: contiguous panel ranges [p0, p1).
+3. **A partitioned.** A rank uploads only the A rows of its panels, in reordered order
+   (``shard_a_rows``), and runs ``bsmr_sddmm_panels_local`` on them.
+4. **B broadcast once** from rank 0 (RCCL), outside the timed region.
+5. **P gathered** by a sum-reduce to rank 0: each output is written by exactly one rank and the
+   others hold 0 there, so the sum is the value exactly.
+
+The timed loop has no collective; the whole-job time is the slowest rank's.
 """
 import os
+import time
 
 import numpy as np
 
@@ -24,11 +41,26 @@ def init(backend):
     return dist.get_rank(), dist.get_world_size()
 
 
-def broadcast_(tensor, src=0):
-    """In-place broadcast (B is generated on rank 0 and sent once, outside the timed region)."""
+def _backend():
     import torch.distributed as dist
 
-    dist.broadcast(tensor, src=src)
+    return dist.get_backend()
+
+
+def _comm(t):
+    """The tensor the collective runs on: gloo has no reduce for device tensors, so it gets a
+    host copy; RCCL takes the device tensor as is."""
+    return t.cpu() if _backend() == "gloo" and t.is_cuda else t
+
+
+def broadcast_(tensor, src=0):
+    """In-place broadcast (e.g. B, generated on rank 0 and sent once before timing)."""
+    import torch.distributed as dist
+
+    c = _comm(tensor)
+    dist.broadcast(c, src=src)
+    if c is not tensor:
+        tensor.copy_(c)
     return tensor
 
 
@@ -38,8 +70,9 @@ def max_over_ranks(value, device):
     import torch.distributed as dist
 
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    c = _comm(t)
+    dist.all_reduce(c, op=dist.ReduceOp.MAX)
+    return float(c.item())
 
 
 def sum_over_ranks(value, device):
@@ -47,11 +80,110 @@ def sum_over_ranks(value, device):
     import torch.distributed as dist
 
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    c = _comm(t)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(c.item())
+
+
+def all_values(value, device):
+    """Every rank's float, in rank order (per-rank times and counts for the report)."""
+    import torch
+    import torch.distributed as dist
+
+    w = dist.get_world_size()
+    t = torch.zeros(w, dtype=torch.float64, device=device)
+    t[dist.get_rank()] = float(value)
+    c = _comm(t)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return [float(x) for x in c.cpu().tolist()]
 
 
 def panel_range(cuts, rank):
-    """Row panels [p0, p1) of `rank` from the cost-model cut points (bsmr.shard_cuts)."""
+    """Row panels [p0, p1) of `rank` from cost-model cut points (bsmr.shard_cuts)."""
     cuts = np.asarray(cuts)
     return int(cuts[rank]), int(cuts[rank + 1])
+
+
+def broadcast_row_stage(hdr, rows, device):
+    """Ship a row stage from rank 0: `hdr` (RowStage) and `rows` (a uint32 numpy array, or a
+    callable that fills the int32 tensor to be sent, e.g. a device-to-device export) on rank 0,
+    anything elsewhere. Returns (hdr, rows tensor int32 on `device`) on every rank.
+
+    The header travels as its bytes, the rows as one device buffer (RCCL reads it in place)."""
+    import torch
+    import torch.distributed as dist
+
+    from . import RowStage
+
+    rank = dist.get_rank()
+    hdr_bytes = torch.zeros(len(bytes(RowStage())), dtype=torch.uint8, device=device)
+    if rank == 0:
+        hdr_bytes.copy_(torch.from_numpy(hdr.to_array()))
+    broadcast_(hdr_bytes, 0)
+    hdr = RowStage.from_array(hdr_bytes.cpu().numpy())
+    out = torch.empty(max(hdr.num_reordered_rows, 1), dtype=torch.int32, device=device)
+    if rank == 0:
+        if callable(rows):
+            rows(out)
+        else:
+            out[:hdr.num_reordered_rows].copy_(
+                torch.from_numpy(np.ascontiguousarray(rows, np.uint32).view(np.int32)))
+    broadcast_(out, 0)
+    return hdr, out
+
+
+def distribute_plan(M, N, rowptr, colidx, device, alpha=0.3, delta=0.3, layout="auto",
+                    free_mem_bytes=0):
+    """The global plan on every rank, clustered once (rank 0) and shipped as its row stage.
+
+    Returns (plan, info): info["plan_build_s"] is rank 0's full plan build, info["distribute_ms"]
+    the row-stage broadcast plus the local column stage (bsmr_plan_import_rows) on this rank.
+    """
+    import torch
+    import torch.distributed as dist
+
+    from . import Plan
+
+    rank = dist.get_rank()
+    dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+    info = {"plan_build_s": 0.0}
+    plan, hdr = None, None
+    if rank == 0:
+        t0 = time.perf_counter()
+        plan = Plan(M, N, rowptr, colidx, alpha=alpha, delta=delta, device=dev.index,
+                    layout=layout, free_mem_bytes=free_mem_bytes)
+        info["plan_build_s"] = time.perf_counter() - t0
+        hdr, _ = plan.export_rows()
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    # rank 0 writes the rows straight into the device buffer the broadcast sends
+    hdr, rows = broadcast_row_stage(hdr, lambda t: plan.export_rows(t.data_ptr()), dev)
+    torch.cuda.synchronize(dev)
+    info["row_stage_bcast_ms"] = (time.perf_counter() - t0) * 1e3
+    info["row_stage_bytes"] = int(len(bytes(hdr)) + 4 * hdr.num_reordered_rows)
+    if rank != 0:
+        plan = Plan.from_row_stage(rowptr, colidx, hdr, rows.data_ptr(), delta=delta,
+                                   device=dev.index, layout=layout)
+    torch.cuda.synchronize(dev)
+    info["distribute_ms"] = (time.perf_counter() - t0) * 1e3
+    return plan, info
+
+
+def shard_a_rows(A, K, reordered_rows, p0, p1):
+    """The A rows of reordered positions [16 p0, min(16 p1, R)) in that order (host, row-major):
+    the dA_local of bsmr_sddmm_panels_local."""
+    A = np.asarray(A).reshape(-1, K)
+    q1 = min(16 * p1, len(reordered_rows))
+    return np.ascontiguousarray(A[np.asarray(reordered_rows[16 * p0:q1], dtype=np.int64)])
+
+
+def gather_p(dP, dst=0):
+    """P in CSR order on rank `dst`: every rank wrote only its panels' outputs into a zeroed
+    nnz buffer, so a sum-reduce assembles P exactly (x + 0 = x). Returns the host array on dst,
+    None elsewhere."""
+    import torch.distributed as dist
+
+    c = _comm(dP)
+    dist.reduce(c, dst=dst, op=dist.ReduceOp.SUM)
+    return c.cpu().numpy() if dist.get_rank() == dst else None

@@ -139,36 +139,79 @@ def cop20k_like(seed=20250802):
 
 def chung_lu(n, nnz_target, seed, exponent=2.2, chunk=20_000_000):
     """Symmetric power-law graph (Chung-Lu): endpoints drawn with probability proportional to
-    w_i = (i+1)^(-1/(exponent-1)); both directions stored, duplicates and self loops dropped."""
+    w_i = (i+1)^(-1/(exponent-1)); self loops dropped, each undirected edge kept once, then both
+    directions stored. Draws continue until nnz_target / 2 distinct edges exist (the heavy rows
+    repeat pairs, so a fixed number of draws falls short), and a seeded sample of exactly that
+    many is kept: the result holds nnz_target stored entries (rounded down to even)."""
     rng = np.random.default_rng(seed)
     w = (np.arange(1, n + 1, dtype=np.float64)) ** (-1.0 / (exponent - 1.0))
     cdf = np.cumsum(w)
     cdf /= cdf[-1]
     perm = rng.permutation(n)
-    keys = []
-    drawn = 0
-    need = int(nnz_target * 0.53)  # undirected draws; duplicates are removed below
-    while drawn < need:
-        m = min(chunk, need - drawn)
-        i = perm[np.searchsorted(cdf, rng.random(m))]
-        j = perm[np.searchsorted(cdf, rng.random(m))]
-        keep = i != j
-        i, j = i[keep], j[keep]
-        keys.append(i.astype(np.int64) * n + j)
-        keys.append(j.astype(np.int64) * n + i)
-        drawn += m
-    key = np.unique(np.concatenate(keys))
-    del keys
+    target = int(nnz_target) // 2
+    edges = np.empty(0, dtype=np.int64)
+    draw, total = int(target * 1.1), 0
+    while True:
+        keys = [edges]
+        drawn = 0
+        while drawn < draw:
+            m = min(chunk, draw - drawn)
+            i = perm[np.searchsorted(cdf, rng.random(m))]
+            j = perm[np.searchsorted(cdf, rng.random(m))]
+            keep = i != j
+            lo = np.minimum(i, j)[keep].astype(np.int64)
+            hi = np.maximum(i, j)[keep].astype(np.int64)
+            keys.append(lo * n + hi)
+            drawn += m
+        total += draw
+        edges = np.unique(np.concatenate(keys))
+        del keys
+        if len(edges) >= target:
+            break
+        # distinct edges per draw fall as the graph fills: ask for the shortfall at the current
+        # yield, plus a margin
+        draw = max(1_000_000, int((target - len(edges)) * 1.5 * total / max(len(edges), 1)))
+    if len(edges) > target:
+        edges = np.sort(rng.choice(edges, size=target, replace=False))
+    lo, hi = edges // n, edges % n
+    del edges
+    key = np.concatenate([lo * n + hi, hi * n + lo])
+    del lo, hi
+    key.sort()
     rowptr = np.zeros(n + 1, dtype=np.int64)
     rowptr[1:] = np.bincount(key // n, minlength=n)
     return n, n, np.cumsum(rowptr).astype(np.uint32), (key % n).astype(np.uint32)
 
 
 def reddit_like(scale=1.0, seed=20250803):
-    """C4 stand-in: 232,965-node power-law graph, ~232M stored entries at scale 1 (BASELINE.json
-    quotes ~232M nnz; the public Reddit graph has 114,615,892 edges). scale < 1 shrinks both."""
+    """C4 stand-in: 232,965-node power-law graph with 232,000,000 stored entries at scale 1
+    (BASELINE.json quotes ~232M nnz: the public Reddit graph's 114,615,892 undirected edges stored
+    in both directions, ~229M). scale < 1 shrinks the nodes by scale and the entries by scale^2."""
     n = max(1024, int(232965 * scale))
     return chung_lu(n, int(232_000_000 * scale * scale), seed)
+
+
+def stack_copies(M, N, rowptr, colidx, copies, seed=20251016):
+    """Weak-scaling workload: `copies` row blocks, block b = the pattern with its columns relabelled
+    by a random permutation of [0, N) (block 0 unchanged), so the blocks' rows are as unlike each
+    other as the pattern's own rows and each block carries the pattern's work. copies = 1 returns
+    the pattern itself."""
+    rowptr = np.asarray(rowptr, dtype=np.uint32)
+    colidx = np.asarray(colidx, dtype=np.uint32)
+    if copies == 1:
+        return M, N, rowptr, colidx
+    rng = np.random.default_rng(seed)
+    nnz = int(rowptr[-1])
+    rp = np.empty(copies * M + 1, dtype=np.uint64)
+    ci = np.empty(copies * nnz, dtype=np.uint32)
+    rp[0] = 0
+    for b in range(copies):
+        perm = np.arange(N, dtype=np.uint32) if b == 0 else rng.permutation(N).astype(np.uint32)
+        rp[1 + b * M: 1 + (b + 1) * M] = rowptr[1:].astype(np.uint64) + b * nnz
+        ci[b * nnz:(b + 1) * nnz] = perm[colidx]
+    if rp[-1] >= 2 ** 32:
+        raise ValueError("stack_copies: more than 2^32 stored entries")
+    return copies * M, N, rp.astype(np.uint32), ci
 
 
 def dlmc_like(kind="uniform", seed=7):

@@ -22,45 +22,28 @@ extern "C" void bsmr_plan_options_default(bsmr_plan_options* o) {
     o->lds_budget_kb = 0;
 }
 
-extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M,
-                                uint32_t N, uint32_t nnz, const bsmr_plan_options* opt,
-                                bsmr_plan** out) {
-    *out = nullptr;
-    if (!rowptr || !colidx || M == 0 || N == 0 || rowptr[M] != nnz || nnz < 2) {
-        set_error("bsmr_plan_create: invalid CSR (need rowptr[M] == nnz >= 2)");
-        return BSMR_ERR_INVALID;
-    }
-    bsmr_plan_options o;
-    if (opt)
-        o = *opt;
-    else
-        bsmr_plan_options_default(&o);
-    auto* h = new bsmr_plan;
-    Plan& p = h->p;
-    auto fail = [&](int st) {
-        delete h;
-        return st;
-    };
+namespace {
+
+// device, stream and the launch / tuning options shared by bsmr_plan_create and
+// bsmr_plan_import_rows
+int init_plan(Plan& p, const bsmr_plan_options& o) {
     p.device = o.device;
     if (hipSetDevice(o.device) != hipSuccess) {
-        set_error("bsmr_plan_create: hipSetDevice failed");
-        return fail(BSMR_ERR_HIP);
+        set_error("bsmr_plan: hipSetDevice failed");
+        return BSMR_ERR_HIP;
     }
     if (hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) != hipSuccess) {
-        set_error("bsmr_plan_create: hipStreamCreate failed");
-        return fail(BSMR_ERR_HIP);
+        set_error("bsmr_plan: hipStreamCreate failed");
+        return BSMR_ERR_HIP;
     }
-    p.M = M;
-    p.N = N;
-    p.nnz = nnz;
     p.alpha = o.alpha;
     p.delta = o.delta;
     p.exact_all = o.exact_similarity;
     if (o.cluster_batch) p.cluster_batch = o.cluster_batch;
     if (o.layout < BSMR_LAYOUT_AUTO || o.layout > BSMR_LAYOUT_COLMAJOR ||
         (o.lds_budget_kb && (o.lds_budget_kb < 16 || o.lds_budget_kb > 160))) {
-        set_error("bsmr_plan_create: bad layout or lds_budget_kb");
-        return fail(BSMR_ERR_INVALID);
+        set_error("bsmr_plan: bad layout or lds_budget_kb");
+        return BSMR_ERR_INVALID;
     }
     p.use_rowblock = o.layout != BSMR_LAYOUT_COLMAJOR;
     p.force_rowblock = o.layout == BSMR_LAYOUT_ROWBLOCK;
@@ -78,6 +61,40 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     if (const char* dk = std::getenv("BSMR_DENSE_KS")) p.dense_ks = std::atoi(dk);
     if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
         p.l2_range_kb = std::max(64, std::atoi(l2));
+    return BSMR_OK;
+}
+
+bool valid_csr(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M, uint32_t N,
+               uint32_t nnz) {
+    return rowptr && colidx && M != 0 && N != 0 && rowptr[M] == nnz && nnz >= 2;
+}
+
+}  // namespace
+
+extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, uint32_t M,
+                                uint32_t N, uint32_t nnz, const bsmr_plan_options* opt,
+                                bsmr_plan** out) {
+    *out = nullptr;
+    if (!valid_csr(rowptr, colidx, M, N, nnz)) {
+        set_error("bsmr_plan_create: invalid CSR (need rowptr[M] == nnz >= 2)");
+        return BSMR_ERR_INVALID;
+    }
+    bsmr_plan_options o;
+    if (opt)
+        o = *opt;
+    else
+        bsmr_plan_options_default(&o);
+    auto* h = new bsmr_plan;
+    Plan& p = h->p;
+    auto fail = [&](int st) {
+        delete h;
+        return st;
+    };
+    p.M = M;
+    p.N = N;
+    p.nnz = nnz;
+    int st = init_plan(p, o);
+    if (st != BSMR_OK) return fail(st);
     u64 free_mem = o.free_mem_bytes;
     if (free_mem == 0) {
         size_t fr = 0, tot = 0;
@@ -95,9 +112,102 @@ extern "C" int bsmr_plan_create(const uint32_t* rowptr, const uint32_t* colidx, 
     p.nbpr = static_cast<u32>(std::ceil(static_cast<float>(N) / static_cast<float>(p.bs)));  // rowReordering.cu:1035
     p.B = cluster_block_dim(p.nbpr);
     p.keptMask = kept_warp_mask(p.B);
-    int st = p.build_rows(rowptr, colidx);
+    st = p.build_rows(rowptr, colidx);
     if (st != BSMR_OK) return fail(st);
     st = p.build_columns();
+    if (st != BSMR_OK) return fail(st);
+    *out = h;
+    return BSMR_OK;
+}
+
+extern "C" int bsmr_plan_export_rows(const bsmr_plan* plan, bsmr_row_stage* hdr, uint32_t* rows) {
+    if (!plan || !hdr) {
+        set_error("bsmr_plan_export_rows: bad arguments");
+        return BSMR_ERR_INVALID;
+    }
+    const Plan& p = plan->p;
+    std::memset(hdr, 0, sizeof(*hdr));
+    hdr->M = p.M;
+    hdr->N = p.N;
+    hdr->nnz = p.nnz;
+    hdr->block_size = p.bs;
+    hdr->num_blocks_per_row = p.nbpr;
+    hdr->cluster_block_dim = p.B;
+    hdr->num_zero_rows = p.z;
+    hdr->num_reordered_rows = p.R;
+    hdr->num_clusters = p.numClusters;
+    hdr->alpha = p.alpha;
+    hdr->row_reorder_ms = p.row_ms;
+    hdr->exact_similarity_evals = p.exact_evals;
+    hdr->total_similarity_evals = p.total_evals;
+    if (rows && p.R) {
+        BSMR_HIP(hipSetDevice(p.device));
+        BSMR_HIP(hipMemcpyAsync(rows, p.rows.data(), static_cast<size_t>(p.R) * sizeof(u32),
+                                hipMemcpyDefault, p.stream));
+        BSMR_HIP(hipStreamSynchronize(p.stream));
+    }
+    return BSMR_OK;
+}
+
+extern "C" int bsmr_plan_import_rows(const uint32_t* rowptr, const uint32_t* colidx,
+                                     const bsmr_row_stage* hdr, const uint32_t* rows,
+                                     const bsmr_plan_options* opt, bsmr_plan** out) {
+    *out = nullptr;
+    if (!hdr || !valid_csr(rowptr, colidx, hdr->M, hdr->N, hdr->nnz) ||
+        hdr->num_reordered_rows > hdr->M || hdr->num_zero_rows > hdr->M ||
+        hdr->num_reordered_rows + hdr->num_zero_rows != hdr->M ||
+        (hdr->num_reordered_rows && !rows)) {
+        set_error("bsmr_plan_import_rows: invalid CSR or row-stage header");
+        return BSMR_ERR_INVALID;
+    }
+    bsmr_plan_options o;
+    if (opt)
+        o = *opt;
+    else
+        bsmr_plan_options_default(&o);
+    o.alpha = hdr->alpha;  // the row stage was built for this alpha; delta comes from opt
+    auto* h = new bsmr_plan;
+    Plan& p = h->p;
+    auto fail = [&](int st) {
+        delete h;
+        return st;
+    };
+    const u32 M = hdr->M, R = hdr->num_reordered_rows;
+    p.M = M;
+    p.N = hdr->N;
+    p.nnz = hdr->nnz;
+    int st = init_plan(p, o);
+    if (st != BSMR_OK) return fail(st);
+    // the rows must be the non-empty rows of S, each once (they index rowptr on the device)
+    std::vector<u32> hrows(R);
+    if (R && hipMemcpy(hrows.data(), rows, static_cast<size_t>(R) * sizeof(u32), hipMemcpyDefault) !=
+                 hipSuccess) {
+        set_error("bsmr_plan_import_rows: cannot read rows");
+        return fail(BSMR_ERR_HIP);
+    }
+    std::vector<uint8_t> seen(M, 0);
+    for (u32 r : hrows) {
+        if (r >= M || seen[r] || rowptr[r] == rowptr[r + 1]) {
+            set_error("bsmr_plan_import_rows: rows are not the non-empty rows of S, each once");
+            return fail(BSMR_ERR_INVALID);
+        }
+        seen[r] = 1;
+    }
+    p.bs = hdr->block_size;
+    p.nbpr = hdr->num_blocks_per_row;
+    p.B = hdr->cluster_block_dim;
+    p.keptMask = kept_warp_mask(p.B);
+    p.z = hdr->num_zero_rows;
+    p.R = R;
+    p.P = (R + 15) / 16;
+    p.numClusters = hdr->num_clusters;
+    p.row_ms = hdr->row_reorder_ms;
+    p.exact_evals = hdr->exact_similarity_evals;
+    p.total_evals = hdr->total_similarity_evals;
+    st = p.rowptr.upload(rowptr, M + 1ull, p.stream);
+    if (st == BSMR_OK) st = p.colidx.upload(colidx, p.nnz, p.stream);
+    if (st == BSMR_OK) st = p.rows.upload(hrows.data(), R, p.stream);  // R >= 1: nnz >= 2
+    if (st == BSMR_OK) st = p.build_columns();
     if (st != BSMR_OK) return fail(st);
     *out = h;
     return BSMR_OK;
@@ -167,8 +277,9 @@ extern "C" int bsmr_plan_get_array(const bsmr_plan* plan, int which, uint32_t* h
         case BSMR_ARR_SPARSE_VALUES: b = &p.sparseValues; n = p.nres; break;
         case BSMR_ARR_SPARSE_RELATIVE_ROWS: b = &p.sparseRel; n = p.nres; break;
         case BSMR_ARR_SPARSE_COL_INDICES: b = &p.sparseColIdx; n = p.nres; break;
-        case BSMR_ARR_DISPERSION: b = &p.disp; n = p.M; break;
-        case BSMR_ARR_ASCENDING: b = &p.asc; n = p.M; break;
+        // (not kept by plans imported from a row stage: length 0)
+        case BSMR_ARR_DISPERSION: b = &p.disp; n = p.disp.n ? p.M : 0; break;
+        case BSMR_ARR_ASCENDING: b = &p.asc; n = p.asc.n ? p.M : 0; break;
         default:
             set_error("bsmr_plan_get_array: unknown array");
             return BSMR_ERR_INVALID;

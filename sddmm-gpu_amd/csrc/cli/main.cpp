@@ -3,8 +3,10 @@
 // with makeData, build the BSMR plan on the GPU, run 10 timed SDDMM iterations, print the log.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -37,12 +39,22 @@ struct Dev {
     ~Dev() { (void)hipFree(p); }
 };
 
-// one reference "sddmm(options, A, B, P, logger)" run on an existing plan (sddmm.cu:10-39)
+// host A (M x K row-major) and B (K x N column-major) of one run
+struct Operands {
+    std::vector<float> A, B;
+};
+
+// one reference "sddmm(options, A, B, P, logger)" run on an existing plan (sddmm.cu:10-39);
+// P_out / ops_out (optional) receive P in CSR order and the operands (validate path)
 void run_sddmm(bsmr_plan* plan, const bsmr_csr* S, uint32_t K, int iters, cli::Logger& log,
-               std::vector<float>* P_out) {
+               std::vector<float>* P_out, Operands* ops_out = nullptr) {
     uint32_t M, N, nnz;
     bsmr_csr_info(S, &M, &N, &nnz);
-    std::vector<float> A(static_cast<size_t>(M) * K), B(static_cast<size_t>(N) * K);
+    Operands ops;
+    std::vector<float>& A = ops.A;
+    std::vector<float>& B = ops.B;
+    A.resize(static_cast<size_t>(M) * K);
+    B.resize(static_cast<size_t>(N) * K);
     bsmr_make_data(A.size(), A.data());  // Matrix<float>(M,K,row_major).makeData()
     bsmr_make_data(B.size(), B.data());  // Matrix<float>(K,N,col_major).makeData()
     Dev dA(A.size() * 4), dB(B.size() * 4), dP(static_cast<size_t>(nnz) * 4);
@@ -76,6 +88,38 @@ void run_sddmm(bsmr_plan* plan, const bsmr_csr* S, uint32_t K, int iters, cli::L
     HIPCHK(hipEventDestroy(e0));
     HIPCHK(hipEventDestroy(e1));
     HIPCHK(hipStreamDestroy(s));
+    if (ops_out) *ops_out = std::move(ops);
+}
+
+// checkSddmm (sddmm.cu:41-59), compiled in by the reference's `#define VALIDATE` (sddmm.cu:7) and
+// switched on here by BSMR_VALIDATE=1 (the flags stay the reference's): host SDDMM of the same
+// operands, checkData's framed report, and the NO PASS line on mismatches.
+// BSMR_VALIDATE_CORRUPT=n (fault injection for tests): add 1 to the first n GPU values first.
+bool check_sddmm(const bsmr_csr* S, uint32_t K, const Operands& ops, std::vector<float>& P) {
+    uint32_t M, N, nnz;
+    bsmr_csr_info(S, &M, &N, &nnz);
+    if (const char* c = std::getenv("BSMR_VALIDATE_CORRUPT")) {
+        const long n = std::min<long>(std::atol(c), static_cast<long>(P.size()));
+        for (long i = 0; i < n; ++i) P[i] += 1.0f;
+    }
+    std::vector<float> Pcpu(nnz);
+    int st = bsmr_sddmm_cpu(bsmr_csr_rowptr(S), bsmr_csr_colidx(S), M, N, K, ops.A.data(),
+                            ops.B.data(), Pcpu.data(), 0);
+    if (st) die("bsmr_sddmm_cpu", st);
+    printf("check cpu sddmm and BSMR sddmm: \n");
+    const uint64_t numError = bsmr_check_data(nnz, Pcpu.data(), P.data(), 1);
+    if (numError) {
+        printf("[checkData : NO PASS Error rate : %2.2f%%]\n",
+               static_cast<double>(static_cast<float>(numError) / static_cast<float>(P.size()) * 100));
+        fflush(stdout);
+        return false;
+    }
+    return true;
+}
+
+bool validate_enabled() {
+    const char* v = std::getenv("BSMR_VALIDATE");
+    return v && v[0] && v[0] != '0';
 }
 
 void fill_plan_fields(bsmr_plan* plan, uint32_t K, cli::Logger& log) {
@@ -191,7 +235,14 @@ int main(int argc, char* argv[]) {
     int st = bsmr_plan_create(bsmr_csr_rowptr(S), bsmr_csr_colidx(S), M, N, nnz, &po, &plan);
     if (st) die("bsmr_plan_create", st);
     fill_plan_fields(plan, K, log);
-    run_sddmm(plan, S, K, options.numIterations(), log, nullptr);
+    if (validate_enabled()) {
+        std::vector<float> P;
+        Operands ops;
+        run_sddmm(plan, S, K, options.numIterations(), log, &P, &ops);
+        check_sddmm(S, K, ops, P);  // printed before the log block, as sddmm() does
+    } else {
+        run_sddmm(plan, S, K, options.numIterations(), log, nullptr);
+    }
     log.print();
     bsmr_plan_destroy(plan);
     bsmr_csr_free(S);

@@ -158,7 +158,8 @@ struct ClusterArgs {
     const u32* S1C;
     u32* state;
     u32* st;
-    u32* ctrl;          // [0] abort, [1] timeout, [2..3] exact evals (u64), [4..5] total evals
+    u32* ctrl;          // [0] abort, [1] timeout, [2..3] exact evals (u64), [4..5] total evals,
+                        // [6] the launch's cluster ticket counter
     u32* cmpScratch;    // [gridDim.x][nbpr] zeros: dense row image of the exact path (global,
                         // so a cluster's LDS is its representative only: more resident clusters)
     u32 M, nbpr, B, keptMask, c0;
@@ -216,11 +217,16 @@ __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
     extern __shared__ __attribute__((aligned(16))) u32 smem[];
     u32* rep = smem;                                                    // nbpr
     float* smn = reinterpret_cast<float*>(smem + ((a.nbpr + 3) & ~3u));  // 32
-    u32* cmp = a.cmpScratch + static_cast<size_t>(blockIdx.x) * a.nbpr;  // zero between uses
     float* smx = smn + 32;
     __shared__ u32 s_abort;
     const u32 l = lane_id();
-    const u32 k = a.c0 + blockIdx.x;
+    // cluster id from a ticket taken at entry, not blockIdx.x: HIP does not promise in-order
+    // workgroup dispatch, and a ticket makes cluster k-1 always started before k waits on it
+    u32 ticket = 0;
+    if (l == 0) ticket = atomicAdd(&a.ctrl[6], 1u);
+    ticket = __shfl(ticket, 0);
+    const u32 k = a.c0 + ticket;
+    u32* cmp = a.cmpScratch + static_cast<size_t>(ticket) * a.nbpr;  // zero between uses
     const u32 M = a.M;
     u64 nexact = 0, ntotal = 0;
     bool aborted = false;
@@ -953,8 +959,8 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
 }
 }  // namespace
 
-const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, bool half, u32 pa, u32 pb,
-                                                  int* err) const {
+std::shared_ptr<const Plan::RowBlockLayout> Plan::rowblock_layout(u32 rowBytes, bool half,
+                                                                  u32 pa, u32 pb, int* err) const {
     *err = BSMR_OK;
     const u32 tmin = half ? tile_min_half : tile_min_f32;
     if (pa == 0 && pb == P) {
@@ -989,16 +995,16 @@ const Plan::RowBlockLayout* Plan::rowblock_layout(u32 rowBytes, bool half, u32 p
                 }
             }
         }
-        return &rb_whole(slot);
+        return std::shared_ptr<const RowBlockLayout>(std::shared_ptr<void>(), &rb_whole(slot));
     }
     for (const auto& L : shard_rbl)
-        if (L->rowBytes == rowBytes && L->pa == pa && L->pb == pb && L->tileMin == tmin) return L.get();
-    auto L = std::make_unique<RowBlockLayout>();
+        if (L->rowBytes == rowBytes && L->pa == pa && L->pb == pb && L->tileMin == tmin) return L;
+    auto L = std::make_shared<RowBlockLayout>();
     *err = build_rowblock_layout(*L, rowBytes, pa, pb, tmin);
     if (*err != BSMR_OK) return nullptr;
     if (shard_rbl.size() >= MAX_SHARD_LAYOUTS) shard_rbl.erase(shard_rbl.begin());
-    shard_rbl.push_back(std::move(L));
-    return shard_rbl.back().get();
+    shard_rbl.push_back(L);
+    return L;
 }
 
 // Row-block launch layout over panels [pa, pb) (the whole plan, or one row-panel shard).
@@ -1403,9 +1409,10 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     ca.exact_all = exact_all;
     ca.timeout_ticks = 100ull * 1000 * 1000 * 20;  // 20 s without progress
     const size_t lds_cl = (((nbpr + 3) & ~3u) + 64) * sizeof(u32);
-    // clusters per launch: a launch's clusters are dispatched in order and each waits only for
-    // its predecessor, so more clusters than fit on the chip at once cannot deadlock (later ones
-    // start as earlier ones finish); capped by the exact path's scratch (<= 256 MiB)
+    // clusters per launch: each workgroup takes the next cluster id from a ticket counter and
+    // waits only for its predecessor, which therefore has always started, so more clusters than
+    // fit on the chip at once cannot deadlock (later ones start as earlier ones finish); capped by
+    // the exact path's scratch (<= 256 MiB)
     const u32 Rmax = static_cast<u32>(std::max<u64>(
         64, std::min<u64>(cluster_batch, (64ull << 20) / std::max<u32>(nbpr, 1))));
     DevBuf<u32> cmpScratch;
@@ -1417,6 +1424,7 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     while (c0 <= M) {  // at most M - z clusters
         const u32 R = std::min<u32>(Rmax, M + 1 - c0);
         ca.c0 = c0;
+        BSMR_HIP(hipMemsetAsync(ctrl.data() + 6, 0, sizeof(u32), s));  // ticket counter
         hipLaunchKernelGGL(k_cluster, dim3(R), dim3(64), lds_cl, s, ca);
         BSMR_HIP(hipGetLastError());
         std::vector<u32> hst(R);

@@ -141,14 +141,17 @@ struct Plan {
     u32 tile_min_f32 = 257, tile_min_half = 128;
     // layouts of panel ranges (row-panel shards, bsmr_sddmm_panels), most recent last
     static constexpr size_t MAX_SHARD_LAYOUTS = 16;
-    mutable std::vector<std::unique_ptr<RowBlockLayout>> shard_rbl;
+    // shared: a caller keeps its layout alive while another thread's request evicts it
+    mutable std::vector<std::shared_ptr<RowBlockLayout>> shard_rbl;
     int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
                               bool orig = false) const;
     // the whole-plan layout a launch of this slot uses (rbl or rblo)
     const RowBlockLayout& rb_whole(int slot) const { return rb_use_orig[slot] ? rblo[slot] : rbl[slot]; }
     // the (cached) layout for rows of rowBytes over panels [pa, pb) for fp32 (half = false) or
-    // fp16/bf16 operands; null on error
-    const RowBlockLayout* rowblock_layout(u32 rowBytes, bool half, u32 pa, u32 pb, int* err) const;
+    // fp16/bf16 operands; null on error. Call with layout_mu held; the whole-plan layouts are
+    // plan members (non-owning pointer), a shard layout is shared with the cache
+    std::shared_ptr<const RowBlockLayout> rowblock_layout(u32 rowBytes, bool half, u32 pa, u32 pb,
+                                                          int* err) const;
 
     mutable DevBuf<uint8_t> tmp;  // scan/sort scratch
     // BSMR_DIAG & 32 debug timeline (4 u64 per wave of the last launch)
@@ -161,6 +164,9 @@ struct Plan {
         return BSMR_OK;
     }
     mutable std::mutex layout_mu;
+    // identity over reordered positions (built on first use): the row list of launches whose A
+    // holds the shard's rows in reordered order (bsmr_sddmm_panels_local)
+    mutable DevBuf<u32> iotaR;
 
     // dense-sampled launch: per 128 x 128 tile of P (original index space) its stored entries
     struct DenseLayout {

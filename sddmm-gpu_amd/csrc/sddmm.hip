@@ -399,6 +399,8 @@ struct RbArgs {
     const u32* rows;
     u32 R, N, RB;  // R: rows at or past this reordered position are not staged (range end)
     u32 qbase;     // reordered position of row block 0 (16 * first panel of the range)
+    u32 row0;      // row staged for positions outside the block (its unused image tail): a row
+                   // the launch's A holds (0, or 16 * first panel for a shard-local A)
     const uint4* items;     // {row block, tile begin, tile end, piece begin}
     const u32* itemEnd;     // piece end
     const uint2* pieces;    // {first entry, column | (length - 1) << 22}
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         const u32 x0 = 64 * ws + lane;
         const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
         if constexpr (MAXB * NR <= 64) {
-            u32 rowv = 0;
+            u32 rowv = a.row0;
             {
                 const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
                 if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
@@ -760,7 +762,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
 #pragma unroll
             for (u32 i = 0; i < MAXB; ++i) {
                 const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
-                src[i] = lr < a.RB && q < a.R ? a.rows[q] : 0u;
+                src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
             }
 #pragma unroll
             for (u32 i = 0; i < MAXB; ++i) {
@@ -899,22 +901,29 @@ bool use_dense(const Plan& p, u32 K, int dtype) {
 
 // the row-block layout of panels [pa, pb) for slot's row size (built on first use)
 int get_rb_layout(const Plan& p, int slot, int dtype, u32 pa, u32 pb,
-                  const Plan::RowBlockLayout** out) {
+                  std::shared_ptr<const Plan::RowBlockLayout>* out) {
     std::lock_guard<std::mutex> g(p.layout_mu);
     int err = BSMR_OK;
     *out = p.rowblock_layout(128u << slot, dtype != BSMR_F32, pa, pb, &err);
     return err;
 }
 
-// mode: 1 = dense tiles only, 2 = residual only, 3 = both (profiling splits)
+// mode: 1 = dense tiles only, 2 = residual only, 3 = both (profiling splits). local: dA holds
+// the rows of reordered positions [16 L.pa, L.rowEnd) in that order (row-panel shard with its
+// own A rows): the launch stages them through the identity row list, from dA shifted back by
+// 16 L.pa rows (addresses only; no row before 16 L.pa is read)
 int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, const void* dB,
-              float* dP, int dtype, u32 mode, hipStream_t s, u32 nb = 1) {
+              float* dP, int dtype, u32 mode, hipStream_t s, u32 nb = 1, bool local = false) {
     if (L.nItems == 0) return BSMR_OK;
     RbArgs a{};
     a.A = static_cast<const char*>(dA);
+    if (local)
+        a.A = reinterpret_cast<const char*>(reinterpret_cast<uintptr_t>(dA) -
+                                            static_cast<uintptr_t>(16ull * L.pa * L.rowBytes));
     a.B = static_cast<const char*>(dB);
     a.P = dP;
-    a.rows = L.orig ? L.rowIds.data() : p.rows.data();
+    a.rows = local ? p.iotaR.data() : L.orig ? L.rowIds.data() : p.rows.data();
+    a.row0 = local ? 16 * L.pa : 0;
     a.R = L.rowEnd;
     a.qbase = L.orig ? 0 : 16 * L.pa;
     a.N = p.N;
@@ -990,7 +999,10 @@ int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout*
     *out = nullptr;
     const int slot = rb_slot(p, K, dtype);
     if (slot < 0) return BSMR_OK;
-    return get_rb_layout(p, slot, dtype, 0, p.P, out);
+    std::shared_ptr<const Plan::RowBlockLayout> L;  // the whole plan's: a plan member
+    BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
+    *out = L.get();
+    return BSMR_OK;
 }
 
 }  // namespace bsmr
@@ -1024,7 +1036,7 @@ extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const
         }
         const int slot = rb_slot(p, K, dtype);
         if (slot >= 0) {
-            const Plan::RowBlockLayout* L = nullptr;
+            std::shared_ptr<const Plan::RowBlockLayout> L;
             BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
             BSMR_CHECK(launch_rb(p, *L, A, B, P, dtype, 3, s, nb));
             continue;
@@ -1063,7 +1075,7 @@ extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const vo
     // the row-block kernel over the range's own layout (same kernel as the whole plan)
     const int slot = rb_slot(p, K, dtype);
     if (slot >= 0) {
-        const Plan::RowBlockLayout* L = nullptr;
+        std::shared_ptr<const Plan::RowBlockLayout> L;  // held until the launch is enqueued
         BSMR_CHECK(get_rb_layout(p, slot, dtype, p0, p1, &L));
         return launch_rb(p, *L, dA, dB, dP, dtype, 3, static_cast<hipStream_t>(stream));
     }
@@ -1095,6 +1107,43 @@ extern "C" int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const vo
     return launch_panels(a, static_cast<hipStream_t>(stream));
 }
 
+extern "C" int bsmr_sddmm_panels_local(const bsmr_plan* plan, const void* dA_local,
+                                       const void* dB, uint32_t K, int dtype, float* dP,
+                                       uint32_t p0, uint32_t p1, void* stream) {
+    if (!plan) {
+        set_error("bsmr_sddmm_panels_local: null plan");
+        return BSMR_ERR_INVALID;
+    }
+    const Plan& p = plan->p;
+    BSMR_CHECK(validate(dA_local, dB, K, dtype, dP));
+    if (p0 > p1 || p1 > p.P) {
+        set_error("bsmr_sddmm_panels_local: bad panel range");
+        return BSMR_ERR_INVALID;
+    }
+    if (p0 == p1) return BSMR_OK;
+    const int slot = rb_slot(p, K, dtype);
+    if (slot < 0) {
+        set_error("bsmr_sddmm_panels_local: needs the row-block launch (rows of 128 B .. 2 KiB)");
+        return BSMR_ERR_UNSUPPORTED;
+    }
+    {
+        std::lock_guard<std::mutex> g(p.layout_mu);
+        if (p.iotaR.size() < p.R) {
+            std::vector<u32> id(p.R);
+            for (u32 q = 0; q < p.R; ++q) id[q] = q;
+            BSMR_CHECK(p.iotaR.upload(id.data(), p.R, p.stream));
+            BSMR_HIP(hipStreamSynchronize(p.stream));
+        }
+    }
+    std::shared_ptr<const Plan::RowBlockLayout> L;  // held until the launch is enqueued
+    BSMR_CHECK(get_rb_layout(p, slot, dtype, p0, p1, &L));
+    if (L->orig)  // the whole range may have picked original-order row blocks: use the
+                  // reordered layout (always built first), whose rows follow the local A
+        L = std::shared_ptr<const Plan::RowBlockLayout>(
+            std::shared_ptr<void>(), &p.rbl[slot + (dtype != BSMR_F32 ? Plan::N_RB_SIZES : 0)]);
+    return launch_rb(p, *L, dA_local, dB, dP, dtype, 3, static_cast<hipStream_t>(stream), 1, true);
+}
+
 extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const void* dB,
                                   uint32_t K, int dtype, float* dP, int iters, void* stream,
                                   float* ms_dense, float* ms_residual, float* ms_total) {
@@ -1105,10 +1154,17 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     const Plan& p = plan->p;
     BSMR_CHECK(validate(dA, dB, K, dtype, dP));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipEvent_t ev[4];
-    for (auto& e : ev) BSMR_HIP(hipEventCreate(&e));
+    struct Events {  // destroyed on every return path
+        hipEvent_t e[4] = {};
+        ~Events() {
+            for (auto& x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } evs;
+    hipEvent_t* ev = evs.e;
+    for (int i = 0; i < 4; ++i) BSMR_HIP(hipEventCreate(&ev[i]));
     const int slot = rb_slot(p, K, dtype);
-    const Plan::RowBlockLayout* L = nullptr;
+    std::shared_ptr<const Plan::RowBlockLayout> L;
     if (slot >= 0) BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
     SddmmArgs full = make_args(p, dA, dB, K, dP);
     full.nd = p.nDenseItems;
@@ -1139,7 +1195,6 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     if (ms_dense) *ms_dense = p.nDenseItems ? t0 / iters : 0.f;
     if (ms_residual) *ms_residual = p.nres ? t1 / iters : 0.f;
     if (ms_total) *ms_total = t2 / iters;
-    for (auto& e : ev) (void)hipEventDestroy(e);
     return BSMR_OK;
 }
 

@@ -1,6 +1,8 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the sharded-run plumbing used by bench.py:
-B broadcast from rank 0, slowest-rank timing, and a disjoint cover of the row panels by the
-cost-model shard cuts. The GPU data path itself has no collective."""
+"""Multi-process (world_size 2, gloo, CPU) tests of the row-panel split bench.py runs on GPUs
+(bsmr/dist.py): the row stage is computed once on rank 0 and broadcast, both ranks
+derive the same panel cuts from the same plan, each rank computes only its panels' outputs from
+its own A rows (shard_a_rows), and a sum-reduce assembles P exactly on rank 0. The per-shard
+compute is the CPU oracle here (no device); the GPU path is tests/test_gpu_shards.py."""
 import os
 import socket
 
@@ -20,46 +22,85 @@ def _free_port():
 def _worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, os.path.join(root, "sddmm-gpu_amd"))
+    sys.path[:0] = [os.path.join(root, "sddmm-gpu_amd"), os.path.join(root, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     import torch
 
     import bsmr
+    import oracle_lib as O
     from bsmr import dist as D
+    from bsmr import synth
 
     r, w = D.init("gloo")
     assert (r, w) == (rank, world)
+    res = {"rank": rank}
     # B broadcast: rank 0 holds the makeData stream, the others receive it
     n = 4096
     B = torch.from_numpy(bsmr.make_data(n)) if rank == 0 else torch.zeros(n)
     D.broadcast_(B, 0)
-    ok_b = bool(np.array_equal(B.numpy(), bsmr.make_data(n)))
-    t = D.max_over_ranks(1.5 + rank, "cpu")
-    # every rank computes the same cuts from the same plan offsets; ranges tile [0, P)
-    bo = np.cumsum([0] + [3, 0, 5, 1, 7, 2, 2, 9, 0, 4]).astype(np.uint32)
-    so = np.cumsum([0] + [100, 40, 0, 900, 10, 10, 300, 0, 5, 77]).astype(np.uint32)
-    cuts = bsmr.shard_cuts(bo, so, 128, w)
+    res["b_ok"] = bool(np.array_equal(B.numpy(), bsmr.make_data(n)))
+    res["t"] = D.max_over_ranks(1.5 + rank, "cpu")
+    res["all"] = D.all_values(10 + rank, "cpu")
+
+    # the weak-scaling workload: 2 stacked copies of a small pattern
+    M0, N, rp0, ci0 = synth.random_rows(300, 2000, 30, seed=41, zipf=1.1, empty_frac=0.05)
+    M, N, rp, ci = synth.stack_copies(M0, N, rp0, ci0, world)
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    alpha, delta, K = np.float32(0.3), np.float32(0.3), 64
+    bs = O.block_size(M, N, 288 * 1024 ** 3)
+    # row stage: clustered on rank 0 only, shipped as (header, rows)
+    hdr, rows = None, None
+    if rank == 0:
+        rows, ncl, _ = O.row_reorder(c, alpha, bs)
+        hdr = bsmr.RowStage(M=M, N=N, nnz=len(ci), block_size=bs,
+                            num_zero_rows=M - len(rows), num_reordered_rows=len(rows),
+                            num_clusters=ncl, alpha=alpha)
+    hdr, rows_t = D.broadcast_row_stage(hdr, rows, "cpu")
+    rows = rows_t.numpy().view(np.uint32)[:hdr.num_reordered_rows].copy()
+    ref_rows, ref_ncl, _ = O.row_reorder(c, alpha, bs)
+    res["rows_ok"] = bool(np.array_equal(rows, ref_rows)) and hdr.num_clusters == ref_ncl
+    # the same plan on both ranks -> the same cuts
+    plan = O.Plan(c, rows, hdr.num_clusters, delta)
+    cuts = bsmr.shard_cuts(plan.array("blockOffsets"), plan.array("sparseValueOffsets"), K, world)
     p0, p1 = D.panel_range(cuts, rank)
-    total = D.sum_over_ranks(p1 - p0, "cpu")
+    res["cut"] = (p0, p1)
+    # this rank's outputs from its own A rows only
+    A = bsmr.make_data(M * K)
+    Bf = bsmr.make_data(N * K)
+    A_local = D.shard_a_rows(A, K, rows, p0, p1)
+    P = np.zeros(len(ci), np.float32)
+    for j, row in enumerate(rows[16 * p0:min(16 * p1, len(rows))]):
+        for e in range(rp[row], rp[row + 1]):
+            P[e] = np.dot(A_local[j].astype(np.float64), Bf[ci[e] * K:(ci[e] + 1) * K])
+    Pg = D.gather_p(torch.from_numpy(P), 0)
+    if rank == 0:
+        ref = O.sddmm_cpu(c, K, A, Bf)
+        res["p_errors"] = O.check_data(ref, Pg)
+        res["p_written"] = int(np.count_nonzero(Pg))
+        res["nnz"] = len(ci)
     import torch.distributed as dist
     dist.destroy_process_group()
-    q.put((rank, ok_b, t, p0, p1, total))
+    q.put(res)
 
 
 @pytest.mark.timeout(300)
-def test_gloo_world2_broadcast_timing_and_shards():
+def test_gloo_world2_row_stage_shards_and_p_gather():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=240) for _ in procs)
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda d: d["rank"])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, b0, t0, a0, a1, tot0), (r1, b1, t1, c0, c1, tot1) = res
-    assert b0 and b1
-    assert t0 == t1 == 2.5
-    assert a0 == 0 and a1 == c0 and c1 == 10 and tot0 == tot1 == 10
+    r0, r1 = res
+    assert r0["b_ok"] and r1["b_ok"]
+    assert r0["t"] == r1["t"] == 2.5
+    assert r0["all"] == r1["all"] == [10.0, 11.0]
+    assert r0["rows_ok"] and r1["rows_ok"]
+    (a0, a1), (b0, b1) = r0["cut"], r1["cut"]
+    assert a0 == 0 and a1 == b0 and a0 < a1 < b1
+    assert r0["p_errors"] == 0 and r0["p_written"] == r0["nnz"]

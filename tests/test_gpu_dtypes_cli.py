@@ -146,11 +146,14 @@ def test_cli_other_formats(tmp_path, fmt):
     else:
         path = str(tmp_path / "s.txt")
         synth.write_snap(path, M, rp, ci)
-    r = subprocess.run([BIN, "-f", path, "-k", "128"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([BIN, "-f", path, "-k", "128"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, BSMR_VALIDATE="1"))
     assert r.returncode == 0, r.stderr
     assert f"sparseMatrix::CSR initialize From file : {path}" in r.stdout
     f = _log_fields(r.stdout)
     assert f["NNZ"] == str(len(ci)) and f["K"] == "128"
+    # the validate path ran (host SDDMM + checkData of the loaded matrix) and passed
+    assert "| Pass! Result validates successfully." in r.stdout
     assert "NO PASS" not in r.stdout
 
 
@@ -198,3 +201,62 @@ def test_half_k1024_rowblock(dtype):
     assert plan.stats()["rb_items"][4] > 0
     ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, Ar, Br)
     assert O.check_data(ref, P) == 0
+
+
+def _oracle_report(n, n_err_vals=None):
+    """checkData's framed text for n values as the oracle prints it (child process: stdout)."""
+    import sys
+    import textwrap
+    code = textwrap.dedent(f"""
+        import sys, numpy as np
+        sys.path[:0] = {sys.path!r}
+        import oracle_lib as O
+        a = np.zeros({n}, np.float32)
+        O.check_data(a, a, verbose=True)
+    """)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                          check=True, timeout=120).stdout
+
+
+@pytest.mark.parametrize("corrupt", [0, 7])
+def test_cli_validate_checkdata_surface(tmp_path, corrupt):
+    """BSMR_VALIDATE=1 (the reference's VALIDATE build, sddmm.cu:34-59): the host SDDMM of the same
+    operands, checkData's framed block before the log, and on a deliberately corrupted P
+    (BSMR_VALIDATE_CORRUPT=n adds 1 to the first n GPU values) the errors and the NO PASS line."""
+    M, N, rp, ci = synth.random_rows(500, 1500, 30, seed=13, zipf=1.05)
+    path = str(tmp_path / "v.mtx")
+    synth.write_mtx(path, M, N, rp, ci)
+    env = dict(os.environ, BSMR_VALIDATE="1")
+    if corrupt:
+        env["BSMR_VALIDATE_CORRUPT"] = str(corrupt)
+    r = subprocess.run([BIN, "-f", path, "-k", "64"], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    head = "check cpu sddmm and BSMR sddmm: \n"
+    assert head in out
+    block = out[out.index(head) + len(head):]
+    block = block[:block.index("|----------------------------------------------------------------|\n") + 67]
+    # the block precedes the log (sddmm() validates before main prints the log)
+    assert out.index(head) < out.index("[bsmr_gflops : ")
+    nnz = len(ci)
+    if not corrupt:
+        assert block == _oracle_report(nnz)
+        assert "NO PASS" not in out
+        return
+    lines = block.splitlines()
+    assert lines[:4] == _oracle_report(nnz).splitlines()[:4]
+    A = make_data(M * 64)
+    B = make_data(N * 64)
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), 64, A, B)
+    errs = [x for x in lines if x.startswith("| Error : idx = ")]
+    assert len(errs) == corrupt
+    for i, x in enumerate(errs):
+        m = re.match(r"\| Error : idx = (\d+), data1 = ([-0-9.]+), data2 = ([-0-9.]+), "
+                     r"difference = ([-0-9.]+)$", x)
+        assert m and int(m.group(1)) == i
+        assert m.group(2) == f"{ref[i]:f}"
+        assert abs(float(m.group(3)) - (ref[i] + 1.0)) < 1e-3
+    rate = np.float32(corrupt) / np.float32(nnz) * np.float32(100)
+    assert f"| No Pass! Inconsistent data! {corrupt} errors! Error rate : {rate:2.2f}%" in lines
+    assert f"[checkData : NO PASS Error rate : {rate:2.2f}%]" in out

@@ -86,12 +86,11 @@ def _gpu_stats(plan):
     }
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("name", ["Trefethen_20000", "Trefethen_20000b", "mycielskian14",
                                   "mycielskian15", "mycielskian16"])
 @pytest.mark.parametrize("alpha", ALPHAS)
 def test_gpu_plan_matches_reference_logs(name, alpha):
-    if name == "mycielskian16" and alpha == 0.9:
-        pytest.skip("12k clusters: covered by the long suite")
     M, N, rp, ci = matrix(name)
     plan = Plan(M, N, rp, ci, alpha=alpha, delta=DELTAS[0], free_mem_bytes=REF_FREE_MEM)
     bad = {}
