@@ -24,7 +24,7 @@ INT_KEYS = [
 ]
 STR_KEYS = ["original_averageDensity", "bsmr_averageDensity", "bsmr_alpha", "bsmr_delta",
             "gridDim_dense", "gridDim_sparse", "bsmr_threadBlockRatio", "bsmr_dataRatio",
-            "sparsity"]
+            "sparsity", "bsmr_gflops", "bsmr_sddmm"]
 
 
 def parse_record(text):
