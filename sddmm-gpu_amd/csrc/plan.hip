@@ -849,6 +849,22 @@ __global__ void k_rb_gather_csr(const u32* __restrict__ order, const u32* __rest
 
 inline u32 grid_for(u64 n, u32 b) { return static_cast<u32>((n + b - 1) / b); }
 
+// staged output: item i's entries [ea, ea + E) sorted by CSR position (keys = positions, vals =
+// index inside the item): slot t of the sorted order -> the entry's metadata low bits, and the
+// position into sortedPos[ea + t]
+__global__ __launch_bounds__(256) void k_item_slots(const uint2* __restrict__ itemEnt,
+                                                    const u32* __restrict__ skeys,
+                                                    const u32* __restrict__ svals,
+                                                    u32* __restrict__ meta,
+                                                    u32* __restrict__ sortedPos) {
+    const uint2 ie = itemEnt[blockIdx.x];
+    for (u32 t = threadIdx.x; t < ie.y; t += blockDim.x) {
+        const u32 j = ie.x + t, e = ie.x + svals[j];
+        meta[e] = (meta[e] & ~0x3FFFFFu) | t;
+        sortedPos[j] = skeys[j];
+    }
+}
+
 // exclusive scan of n values into out[0..n] (out[n] = total)
 int excl_scan(const u32* in, u32* out, u32 n, DevBuf<uint8_t>& tmp, hipStream_t s) {
     BSMR_HIP(hipMemsetAsync(out, 0, sizeof(u32), s));
@@ -1219,7 +1235,14 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     std::vector<double> cu(nRB, 0.0);
     for (u32 b = 0; b < nRB; ++b) cu[b] = split[b] ? 0.0 : cb[b];
     const std::vector<u32> nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u);
+    // staged output: the LDS past the A image (the launch takes 160 / 80 KiB) holds an item's
+    // results when it has room for >= 1024 of them; larger items are cut to fit
+    const size_t ldsDyn = (NT == 1024 ? 160u : 80u) * 1024u;
+    const u32 outCap = ldsDyn > lds ? static_cast<u32>((ldsDyn - lds) / 4) : 0u;
+    const bool staged = outCap >= 1024 && (out_staged == 1 || (out_staged == -1 &&
+                                                              4ull * nnz > out_staged_min));
     auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch) {
+        if (staged) nch = std::max<u32>(nch, (ne + outCap - 1) / outCap);
         for (u32 k = 0; k < nch; ++k) {
             const u32 ea = e0 + static_cast<u32>(static_cast<u64>(ne) * k / nch);
             const u32 eb = e0 + static_cast<u32>(static_cast<u64>(ne) * (k + 1) / nch);
@@ -1289,6 +1312,10 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // (piece_order 1: all items of an XCD would sweep their column range together)
     const u32 G = rowBytes >= 2048 ? 16 : rowBytes >= 1024 ? 8 : 4;  // sddmm.hip RowGeom (128..512: 4)
     const u32 NG = piece_order == 1 ? NT / G : 0xFFFFFFFFu;  // sort window
+    std::vector<uint2> ient(items.size());
+    for (size_t i = 0; i < items.size(); ++i)
+        ient[i] = make_uint2(items[i].w, (items[i].y == items[i].z && items[i].w == ends[i]) ? 0u
+                                                                                          : ends[i] - items[i].w);
     std::vector<uint2> pieces;
     pieces.reserve(n / 4 + items.size());
     std::vector<uint2> mine;
@@ -1321,6 +1348,49 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     }
     L.nItems = static_cast<u32>(items.size());
     L.nPieces = static_cast<u32>(pieces.size());
+    L.outLds = 0;
+    L.outCap = 0;
+    L.sortedPos.release();
+    L.itemEnt.release();
+    if (staged && n) {
+        // slots: per item, its entries sorted by CSR position (segmented radix sort on the device)
+        BSMR_CHECK(L.itemEnt.upload(ient.data(), ient.size(), s));
+        std::vector<u32> segb(ient.size()), sege(ient.size());
+        for (size_t i = 0; i < ient.size(); ++i) {
+            segb[i] = ient[i].x;
+            sege[i] = ient[i].x + ient[i].y;
+        }
+        DevBuf<u32> dsb, dse, lidx, skeys, svals;
+        BSMR_CHECK(dsb.upload(segb.data(), segb.size(), s));
+        BSMR_CHECK(dse.upload(sege.data(), sege.size(), s));
+        std::vector<u32> hl(n);
+        for (size_t i = 0; i < ient.size(); ++i)
+            for (u32 t = 0; t < ient[i].y; ++t) hl[ient[i].x + t] = t;
+        BSMR_CHECK(lidx.upload(hl.data(), n, s));
+        BSMR_CHECK(skeys.alloc(n));
+        BSMR_CHECK(svals.alloc(n));
+        // entries outside every item (none) keep their place: pre-fill the outputs with the input
+        BSMR_HIP(hipMemcpyAsync(skeys.data(), L.out.data(), n * sizeof(u32), hipMemcpyDeviceToDevice, s));
+        BSMR_HIP(hipMemcpyAsync(svals.data(), lidx.data(), n * sizeof(u32), hipMemcpyDeviceToDevice, s));
+        size_t bytes = 0;
+        const int endbit = bits_for(nnz);
+        BSMR_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, bytes, L.out.data(), skeys.data(), lidx.data(), svals.data(), static_cast<int>(n),
+            static_cast<int>(ient.size()), dsb.data(), dse.data(), 0, endbit, s));
+        if (bytes > tmp.size()) BSMR_CHECK(tmp.alloc(bytes));
+        BSMR_HIP(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            tmp.data(), bytes, L.out.data(), skeys.data(), lidx.data(), svals.data(),
+            static_cast<int>(n), static_cast<int>(ient.size()), dsb.data(), dse.data(), 0, endbit, s));
+        BSMR_CHECK(L.sortedPos.alloc(n));
+        hipLaunchKernelGGL(k_item_slots, dim3(static_cast<u32>(ient.size())), dim3(256), 0, s,
+                           L.itemEnt.data(), skeys.data(), svals.data(), L.meta.data(),
+                           L.sortedPos.data());
+        BSMR_HIP(hipGetLastError());
+        BSMR_HIP(hipStreamSynchronize(s));
+        L.out.release();
+        L.outLds = static_cast<u32>(lds);
+        L.outCap = outCap;
+    }
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
     BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));
     BSMR_CHECK(L.pieces.upload(pieces.data(), std::max<size_t>(pieces.size(), 1), s));

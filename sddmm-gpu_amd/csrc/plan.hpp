@@ -48,6 +48,13 @@ struct Plan {
     u32 l2_range_kb = 2048;
     // entries per column-run piece of the row-block layout (<= RB_PIECE_MAX; BSMR_PIECE_MAX)
     u32 piece_max = RB_PIECE_MAX;
+    // row-block results staged in LDS and written in CSR order per item, for P larger than
+    // out_staged_min bytes (BSMR_OUT_STAGED: 0 never, 1 always, else auto). Measured
+    // (profiles/r02ab1): C3 cop20k-like (P 10 MB) 77.0 -> 72.0 us, C4 reddit-like x0.5 (232 MB)
+    // 1.394 -> 1.305 ms; C2 nips-like (3 MB, P stays in L2 and its scattered stores merge there)
+    // 11.86 -> 12.60 us, so it stays on one store per entry
+    int out_staged = -1;
+    u64 out_staged_min = 8ull << 20;
     // fp16/bf16 patterns with at least this fraction of M x N stored run the dense-sampled
     // launch (whole 128 x 128 MFMA tiles; BSMR_DENSE_MIN; > 1 = never). Measured crossover
     // (tools/dense_sweep.py, 2048^2 bf16 K=512): gathered faster at 3 %, dense from 5 %
@@ -106,8 +113,17 @@ struct Plan {
         u32 tileMin = 0, nTilesKept = 0, nDemoted = 0, nEntries = 0, nWorkItems = 0;
         DevBuf<u32> tileIds;  // kept tile ids; item tile ranges index this list
         size_t lds = 0;
-        DevBuf<u32> meta;   // local row << 22 | column
-        DevBuf<u32> out;    // output index (CSR position)
+        DevBuf<u32> meta;   // local row << 22 | column (staged output: local row << 22 | slot)
+        DevBuf<u32> out;    // output index (CSR position); released when the output is staged
+        // staged output (outLds != 0): an item's results go to LDS at byte offset outLds, slot =
+        // the entry's rank by CSR position inside its item, and the workgroup writes them at the
+        // end in CSR order (P[sortedPos[ea + t]] = slot t: runs of consecutive positions become
+        // full-line stores instead of one scattered 4-byte store per entry). itemEnt[i] = {ea,
+        // number of entries} of item i; entries of an item never exceed the LDS tail past the
+        // A image (outCap floats)
+        u32 outLds = 0, outCap = 0;
+        DevBuf<u32> sortedPos;
+        DevBuf<uint2> itemEnt;
         DevBuf<uint4> items;
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}

@@ -411,6 +411,12 @@ struct RbArgs {
     const u32* denseCols;
     const u32* blockValues;
     u32 mode;  // 1 = dense tiles, 2 = residual, 3 = both
+    // staged output (Plan::RowBlockLayout::outLds): != 0 = byte offset of the item's result slots
+    // in LDS; the entry metadata's low bits are then the slot, and the workgroup writes the slots
+    // to P[sortedPos[itemEnt.x + t]] at the end
+    u32 outLds;
+    const u32* sortedPos;
+    const uint2* itemEnt;
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
@@ -606,7 +612,10 @@ __device__ __forceinline__ void load_piece(const RbArgs& a, const u32 pi, const 
     for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
         const u32 e = G * k + sub;
         pc.mm[k] = e < pc.len ? a.meta[pc.first + e] : 0u;
-        pc.mo[k] = e < pc.len ? a.out[pc.first + e] : 0u;
+        if (a.outLds)
+            pc.mo[k] = pc.mm[k] & 0x3FFFFFu;  // the slot
+        else
+            pc.mo[k] = e < pc.len ? a.out[pc.first + e] : 0u;
     }
 }
 
@@ -672,7 +681,12 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             if constexpr (G == 16) sm += dppf<0x140>(sm);  // row_mirror: the other half-row
             if (sub == static_cast<u32>(i)) res = sm;
         }
-        if (sub < nb) a.P[pc.mo[k]] = res;
+        if (sub < nb) {
+            if (a.outLds)
+                *reinterpret_cast<float*>(const_cast<char*>(As) + a.outLds + 4 * pc.mo[k]) = res;
+            else
+                a.P[pc.mo[k]] = res;
+        }
     }
 }
 
@@ -807,6 +821,12 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         dt.load(a, a.tileIds[t], q0, tb);
         dt.run(a, As, tb);
     }
+    if (a.outLds) {  // the item's results in CSR order: runs of consecutive positions
+        __syncthreads();
+        const uint2 ie = a.itemEnt[blockIdx.x];
+        const float* res = reinterpret_cast<const float*>(As + a.outLds);
+        for (u32 t = tid; t < ie.y; t += NT) a.P[a.sortedPos[ie.x + t]] = res[t];
+    }
     trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
 }
 
@@ -933,6 +953,9 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.pieces = L.pieces.data();
     a.meta = L.meta.data();
     a.out = L.out.data();
+    a.outLds = (mode & 2) ? L.outLds : 0u;  // (dense-only profiling launches write no slots)
+    a.sortedPos = L.sortedPos.data();
+    a.itemEnt = L.itemEnt.data();
     a.tilePanel = p.denseItems.data();
     a.tileIds = L.tileIds.data();
     a.denseCols = p.denseCols.data();

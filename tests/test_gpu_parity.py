@@ -231,6 +231,13 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     ({"BSMR_ORIG_ROWS": "1"}, 256, 1),
     ({"BSMR_ORIG_ROWS": "1"}, 32, 0),
     ({"BSMR_ORIG_ROWS": "1", "BSMR_L2_RANGE_KB": "64"}, 128, 0),
+    # results staged in LDS, written per item in CSR order (auto for P > 8 MiB)
+    ({"BSMR_OUT_STAGED": "1"}, 128, 0),
+    ({"BSMR_OUT_STAGED": "1"}, 32, 0),
+    ({"BSMR_OUT_STAGED": "1"}, 256, 1),
+    ({"BSMR_OUT_STAGED": "1", "BSMR_TILE_MIN_HALF": "0"}, 512, 2),
+    ({"BSMR_OUT_STAGED": "1", "BSMR_ORIG_ROWS": "1"}, 128, 0),
+    ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "64", "BSMR_TILE_MIN_F32": "0"}, 64, 0),
 ])
 def test_rowblock_layout_variants(monkeypatch, env, K, dtype):
     """Launch-layout switches (tile demotion thresholds, L2 column ranges, piece order) on the

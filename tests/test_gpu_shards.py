@@ -103,10 +103,13 @@ def _run_local(plan, rows, A, B, K, nnz, shards, dtype):
     ("zipf", 512, 2, 2), ("blocky", 256, 1, 2), ("banded", 128, 0, 1), ("banded", 256, 1, 2),
     ("zipf", 512, 0, 5),
 ])
-def test_panels_local_every_output_once(name, K, dtype, world):
+@pytest.mark.parametrize("staged", ["0", "1"])
+def test_panels_local_every_output_once(monkeypatch, name, K, dtype, world, staged):
     """Each shard writes exactly its panels' entries from its own A rows (NaN elsewhere stays
     NaN); together they equal the oracle. world 1 on the banded case: the whole range, whose
-    plan-wide layout uses original-order row blocks, runs the reordered layout instead."""
+    plan-wide layout uses original-order row blocks, runs the reordered layout instead. staged:
+    results through LDS in CSR order (BSMR_OUT_STAGED) or one store per entry."""
+    monkeypatch.setenv("BSMR_OUT_STAGED", staged)
     M, N, rp, ci = _cases()[name]
     # (the blocky mask is tile-dominated: its auto launch is column-major, so force row blocks)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--lds-kb", type=int, default=0)
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
+    ap.add_argument("--mask", default=None, help="dlmc_like mask: uniform | block")
     ap.add_argument("--diag", type=int, default=0, help="BSMR_DIAG ablation bits (sddmm.hip)")
     args = ap.parse_args()
     if args.diag:
@@ -34,7 +35,10 @@ def main():
     from bsmr import Plan, make_data, synth
 
     gen = getattr(synth, args.workload)
-    M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
+    if args.mask is not None:
+        M, N, rp, ci = gen(args.mask)
+    else:
+        M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
     K = args.K
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout,
                 lds_budget_kb=args.lds_kb)
