@@ -47,7 +47,10 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
     }
     p.use_rowblock = o.layout != BSMR_LAYOUT_COLMAJOR;
     p.force_rowblock = o.layout == BSMR_LAYOUT_ROWBLOCK;
-    if (o.lds_budget_kb) p.rb_lds_kb = o.lds_budget_kb;
+    if (o.lds_budget_kb) {
+        p.rb_lds_kb = o.lds_budget_kb;
+        p.rb_lds_user = true;
+    }
     if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
     if (const char* po = std::getenv("BSMR_PIECE_ORDER")) p.piece_order = static_cast<u32>(std::atoi(po));
     if (const char* tm = std::getenv("BSMR_TILE_MIN_F32")) p.tile_min_f32 = static_cast<u32>(std::atoi(tm));
@@ -61,8 +64,10 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
     if (const char* dk = std::getenv("BSMR_DENSE_KS")) p.dense_ks = std::atoi(dk);
     if (const char* os = std::getenv("BSMR_OUT_STAGED"))  // "0" never, "1" always, else auto
         p.out_staged = os[0] == '0' ? 0 : os[0] == '1' ? 1 : -1;
-    if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB"))
+    if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB")) {
         p.l2_range_kb = std::max(64, std::atoi(l2));
+        p.l2_range_user = true;
+    }
     return BSMR_OK;
 }
 

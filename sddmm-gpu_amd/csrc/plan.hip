@@ -1045,7 +1045,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 ebase = orig ? 0 : h_sparseValueOffsets[pa];
     // residual entries of the range (original order: every stored entry)
     const u32 n0 = orig ? nnz : h_sparseValueOffsets[pb] - ebase;
-    u32 RBr = rowblock_rows(rowBytes, rb_lds_kb, Rs);
+    // staged output (results through LDS, written per item in CSR order) for large P
+    const bool stagedWanted = out_staged == 1 || (out_staged == -1 && 4ull * nnz > out_staged_min);
+    const u32 ldsKb = stagedWanted && !rb_lds_user ? rb_lds_kb_staged : rb_lds_kb;
+    const u32 l2Kb = stagedWanted && !l2_range_user ? l2_range_kb_staged : l2_range_kb;
+    u32 RBr = rowblock_rows(rowBytes, ldsKb, Rs);
     {
         // sparse rows (< 64 stored entries per row: banded / FEM patterns) keep their row blocks
         // whole, one item each; when there are more row blocks than workgroup slots, use the
@@ -1146,7 +1150,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // column run, from L2 instead of the Infinity Cache)
     constexpr u32 CM = (1u << 22) - 1;
     const u32 m = std::max<u32>(1, static_cast<u32>(std::ceil(
-        static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(l2_range_kb) * 1024.0))));
+        static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(l2Kb) * 1024.0))));
     const u32 NCR = XCD_BUCKETS * m;
     std::vector<u32> cuts(NCR + 1, N);
     cuts[0] = 0;
@@ -1239,8 +1243,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // results when it has room for >= 1024 of them; larger items are cut to fit
     const size_t ldsDyn = (NT == 1024 ? 160u : 80u) * 1024u;
     const u32 outCap = ldsDyn > lds ? static_cast<u32>((ldsDyn - lds) / 4) : 0u;
-    const bool staged = outCap >= 1024 && (out_staged == 1 || (out_staged == -1 &&
-                                                              4ull * nnz > out_staged_min));
+    const bool staged = stagedWanted && outCap >= 1024;
     auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch) {
         if (staged) nch = std::max<u32>(nch, (ne + outCap - 1) / outCap);
         for (u32 k = 0; k < nch; ++k) {

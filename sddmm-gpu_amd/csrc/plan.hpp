@@ -40,12 +40,19 @@ struct Plan {
     bool use_rowblock = true;
     bool force_rowblock = false;  // BSMR_LAYOUT_ROWBLOCK: also for tile-dominated plans
     u32 rb_lds_kb = 144;  // LDS budget of a row-block workgroup (bsmr_plan_options.lds_budget_kb)
+    bool rb_lds_user = false;  // set by the caller: then also for staged layouts
+    // staged-output layouts (below) default to a 120 KiB image and 4 MiB column ranges: the
+    // 40 KiB tail holds 10240 results, so items are cut less, and each row block is staged for
+    // half as many ranges. C4 reddit-like x0.5 sweep (profiles/r02abl/C4_sweep*.txt): 1.305 ms at
+    // (144 KiB, 2 MiB) -> 1.128 ms at (120 KiB, 4 MiB); C3 unchanged (72.9-73.2 us)
+    u32 rb_lds_kb_staged = 120, l2_range_kb_staged = 4096;
     u32 diag = 0;  // BSMR_DIAG profiling ablations (wrong results; never set in normal use)
     // row-block piece order inside an item (tuning experiments: BSMR_PIECE_ORDER): 0 = longest
     // first over the whole item, 1 = column windows of one phase, longest first inside
     u32 piece_order = 0;
     // L2 budget of one column range of the row-block layout (KiB; BSMR_L2_RANGE_KB)
     u32 l2_range_kb = 2048;
+    bool l2_range_user = false;  // BSMR_L2_RANGE_KB given: then also for staged layouts
     // entries per column-run piece of the row-block layout (<= RB_PIECE_MAX; BSMR_PIECE_MAX)
     u32 piece_max = RB_PIECE_MAX;
     // row-block results staged in LDS and written in CSR order per item, for P larger than

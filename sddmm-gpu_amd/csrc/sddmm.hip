@@ -583,7 +583,9 @@ template <int RBY>
 __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const u32 sub,
                                           const u32 (&rot)[RowGeom<RBY>::NC],
                                           f32x4 (&bv)[RowGeom<RBY>::NC]) {
-    const u32 bb = col * RBY + 16 * sub;  // B < 4 GiB on this path (rb_slot)
+    // B < 4 GiB on this path (rb_slot); BSMR_DIAG & 64 (ablation only): every piece reads
+    // column 0, so the B gathers hit L2
+    const u32 bb = ((a.diag & 64) ? 0u : col) * RBY + 16 * sub;
 #pragma unroll
     for (u32 f = 0; f < RowGeom<RBY>::NC; ++f)
         bv[f] = f + RowGeom<RBY>::RR <= RowGeom<RBY>::NC
@@ -825,7 +827,25 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         __syncthreads();
         const uint2 ie = a.itemEnt[blockIdx.x];
         const float* res = reinterpret_cast<const float*>(As + a.outLds);
-        for (u32 t = tid; t < ie.y; t += NT) a.P[a.sortedPos[ie.x + t]] = res[t];
+        if (!(a.diag & 128)) {  // (BSMR_DIAG & 128, ablation only: no P stores)
+            // eight position loads in flight per lane before their stores: a loop of dependent
+            // load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5: 1.135 ->
+            // 1.082 ms). Issuing the first batch before the barrier measured slower (1.109 ms)
+            constexpr u32 U = 8;
+            for (u32 t0 = tid; t0 < ie.y; t0 += U * NT) {
+                u32 pos[U];
+#pragma unroll
+                for (u32 k = 0; k < U; ++k) {
+                    const u32 t = t0 + k * NT;
+                    pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
+                }
+#pragma unroll
+                for (u32 k = 0; k < U; ++k) {
+                    const u32 t = t0 + k * NT;
+                    if (t < ie.y) a.P[pos[k]] = res[t];
+                }
+            }
+        }
     }
     trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
 }
