@@ -4,7 +4,7 @@
 //   1. k_encode        per-row LDS histogram of col/bs -> sparse encoding, dispersion, norms
 //                      [kernel::calculateDispersion, rowReordering.cu:49-93, 478-501]
 //   2. radix sort      rows stably by dispersion [host::sort_by_key, rowReordering.cu:1055-1062]
-//   3. k_cluster       similarity clustering as a persistent chain of wave-sized workgroups
+//   3. k_cluster       similarity clustering as a persistent chain of cluster tiles
 //                      [bsa_clustering + get_permutation_gpu, rowReordering.cu:215-432, 893-1007]
 //   4. radix sort      positions stably by cluster id -> reorderedRows [rowReordering.cu:988-996,
 //                      1081-1090]
@@ -134,12 +134,20 @@ __global__ void k_init_state(u32* state, u32* st, u32 M, u32 z) {
 // ------------------------------------------------------------------------------------------
 // 3. Clustering. The reference runs one single-block kernel per cluster and chains them with
 // per-row device mutexes and device-side launches; the result is sequential first-fit (cluster
-// c examines position i only after c-1 has). Here every cluster is one wave-sized workgroup of
-// a persistent launch; cluster k follows cluster k-1 through the per-position state word:
+// c examines position i only after c-1 has, and takes it when the similarity to its
+// representative exceeds alpha). Here one 1024-thread workgroup runs a TILE of T consecutive
+// clusters (T representatives side by side in LDS): every candidate position's encoding is read
+// once per tile instead of once per cluster, and the 16 waves evaluate 16 positions at a time
+// against all T representatives. A leader wave then walks the sub-batch in position order and
+// applies the sequential rule: position p goes to the first tile cluster whose similarity
+// exceeds alpha; while the tile has fewer than T clusters, a position no cluster takes starts
+// the next one; once it is full, a position every cluster rejects is passed on. An accept or a
+// new cluster changes a representative, so the positions after it are evaluated again (both
+// are rare next to rejects). Tiles follow each other through the per-position state word:
 //     state[i] = ASSIGNED | c   row assigned to cluster c (sticky)
 //     state[i] = c              unassigned, rejected by clusters 1..c
-// and k-1 publishes its start in st[k-1] (start + 2; ST_NONE = no such cluster). A launch runs
-// `R` consecutive clusters; the next launch continues from the last one's start.
+// and cluster c publishes its start in st[c] (start + 2; ST_NONE = no such cluster). A launch
+// runs R = T x (tiles) consecutive clusters; the next launch continues from the last one.
 //
 // Similarity: calculate_similarity_norm_weighted_jaccard (rowReordering.cu:235-293) with the
 // reference's reduce_sum tree (cudaUtil.cuh:13-45) for block size B: each logical thread t<B
@@ -159,30 +167,53 @@ struct ClusterArgs {
     u32* state;
     u32* st;
     u32* ctrl;          // [0] abort, [1] timeout, [2..3] exact evals (u64), [4..5] total evals,
-                        // [6] the launch's cluster ticket counter
-    u32* cmpScratch;    // [gridDim.x][nbpr] zeros: dense row image of the exact path (global,
-                        // so a cluster's LDS is its representative only: more resident clusters)
-    u32 M, nbpr, B, keptMask, c0;
+                        // [6] the launch's tile ticket counter
+    u32* cmpScratch;    // [tiles][nbpr] zeros: dense row image of the exact path
+    u32 M, nbpr, NP, B, keptMask, c0, T;
     float alpha;
     int exact_all;
     u64 timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
 
 constexpr double GUARD = 1e-5;
+constexpr u32 CL_TMAX = 8;      // clusters per tile (register arrays)
+constexpr u32 CL_WAVES = 16;    // waves per tile workgroup
+constexpr u32 CL_SUB = 64;      // positions per evaluation sub-batch (4 per wave)
+constexpr u32 CL_WIN = 256;     // ready positions per window
+constexpr u32 CL_LDS_BUDGET = 148 * 1024;  // representatives (the control block follows)
+// evaluation codes (per position, per sub-batch): the tile cluster where the walk stopped
+constexpr u32 EV_REJECT = 0xFFu, EV_ACCEPT = 0x100u, EV_EXACT = 0x200u;
 
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
-// exact fp32 similarity, all 64 lanes, rep/cmp dense in LDS
-__device__ float sim_exact(const u32* rep, const u32* cmp, u32 nbpr, u32 B, u32 keptMask,
-                           float nr, float nc, float* smn, float* smx) {
+// control block after the representatives
+struct ClusterCtl {
+    u32 todo[CL_WIN];      // unassigned ready positions of the window
+    u32 res[CL_WIN];       // evaluation code per todo slot (current sub-batch)
+    uint4 meta[CL_WIN];    // per todo slot: encoding offset, #blocks, SC, S1C of its row
+    float inrf[CL_TMAX];   // 1 / nr per tile cluster (0 for an empty or zero-norm slot)
+    float nr[CL_TMAX];     // sqrtf(SR)
+    u32 SR[CL_TMAX];       // kept-block sum of squares of the representative (u32 wrap)
+    u64 S1R[CL_TMAX];      // kept-block sum of the representative
+    u32 ntodo, t, nact, done, i;
+    u64 nexact, ntotal;
+};
+
+// exact fp32 similarity of a tile cluster (LDS, element i at rep[i * TS]) with the row whose
+// dense image is cmp (global scratch), one wave; the warp partials live in lanes 0..31 and the
+// strided tree is applied lane-parallel (each level reads only indices the level does not write)
+template <u32 TS>
+__device__ float sim_exact_wave(const u32* rep, const u32* cmp, u32 nbpr, u32 B, float nr,
+                                float nc) {
     const u32 l = lane_id();
     const u32 J = (B + 63) / 64;
+    float wmn = 0.0f, wmx = 0.0f;
     for (u32 j = 0; j < J; ++j) {
         const u32 t = l + 64 * j;
         float pm = 0.0f, px = 0.0f;
         if (t < B) {
             for (u32 i = t; i < nbpr; i += B) {
-                const float x = static_cast<float>(rep[i]) / nr;
+                const float x = static_cast<float>(rep[i * TS]) / nr;
                 const float y = static_cast<float>(cmp[i]) / nc;
                 pm = pm + fminf(x, y);
                 px = px + fmaxf(x, y);
@@ -193,43 +224,185 @@ __device__ float sim_exact(const u32* rep, const u32* cmp, u32 nbpr, u32 B, u32 
             pm = pm + __shfl_xor(pm, o);
             px = px + __shfl_xor(px, o);
         }
-        if ((l & 31) == 0 && t < B) {
-            smn[t >> 5] = pm;
-            smx[t >> 5] = px;
+        // warp 2j = lanes 0-31, warp 2j+1 = lanes 32-63
+        const float m0 = __shfl(pm, 0), m1 = __shfl(pm, 32);
+        const float x0 = __shfl(px, 0), x1 = __shfl(px, 32);
+        if (l == 2 * j) {
+            wmn = m0;
+            wmx = x0;
+        }
+        if (l == 2 * j + 1) {
+            wmn = m1;
+            wmx = x1;
         }
     }
-    __syncthreads();
-    float sim = 0.0f;
-    if (l == 0) {
-        for (u32 stride = B / 64; stride >= 1; stride >>= 1)
-            for (u32 w = 0; w < stride; ++w) {
-                smn[w] = smn[w] + smn[w + stride];
-                smx[w] = smx[w] + smx[w + stride];
-            }
-        sim = smn[0] / smx[0];
+    for (u32 stride = B / 64; stride >= 1; stride >>= 1) {
+        const float on = __shfl(wmn, (l + stride) & 63), ox = __shfl(wmx, (l + stride) & 63);
+        if (l < stride) {
+            wmn = wmn + on;
+            wmx = wmx + ox;
+        }
     }
-    __syncthreads();
-    (void)keptMask;
-    return __shfl(sim, 0);
+    const float mn0 = __shfl(wmn, 0), mx0 = __shfl(wmx, 0);
+    return mn0 / mx0;
 }
 
-__global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
-    extern __shared__ __attribute__((aligned(16))) u32 smem[];
-    u32* rep = smem;                                                    // nbpr
-    float* smn = reinterpret_cast<float*>(smem + ((a.nbpr + 3) & ~3u));  // 32
-    float* smx = smn + 32;
-    __shared__ u32 s_abort;
+__device__ __forceinline__ double readlane_f64(double v, u32 lane) {
+    const u64 b = __builtin_bit_cast(u64, v);
+    const u32 lo = __builtin_amdgcn_readlane(static_cast<u32>(b), lane);
+    const u32 hi = __builtin_amdgcn_readlane(static_cast<u32>(b >> 32), lane);
+    return __builtin_bit_cast(double, (static_cast<u64>(hi) << 32) | lo);
+}
+
+// the 8 per-lane partial sums reduced over the wave together (transposed butterfly: each xor
+// step halves the values a lane keeps); cluster c's total ends in lanes 8c .. 8c + 7
+__device__ __forceinline__ double wave_sum8(const double (&v)[CL_TMAX]) {
     const u32 l = lane_id();
-    // cluster id from a ticket taken at entry, not blockIdx.x: HIP does not promise in-order
-    // workgroup dispatch, and a ticket makes cluster k-1 always started before k waits on it
-    u32 ticket = 0;
-    if (l == 0) ticket = atomicAdd(&a.ctrl[6], 1u);
-    ticket = __shfl(ticket, 0);
-    const u32 k = a.c0 + ticket;
+    double a4[4], a2[2];
+    const bool b5 = (l & 32) != 0, b4 = (l & 16) != 0, b3 = (l & 8) != 0;
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+        const double keep = b5 ? v[4 + i] : v[i], send = b5 ? v[i] : v[4 + i];
+        a4[i] = keep + __shfl_xor(send, 32);
+    }
+#pragma unroll
+    for (u32 i = 0; i < 2; ++i) {
+        const double keep = b4 ? a4[2 + i] : a4[i], send = b4 ? a4[i] : a4[2 + i];
+        a2[i] = keep + __shfl_xor(send, 16);
+    }
+    double s;
+    {
+        const double keep = b3 ? a2[1] : a2[0], send = b3 ? a2[0] : a2[1];
+        s = keep + __shfl_xor(send, 8);
+    }
+    s += __shfl_xor(s, 4);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 1);
+    return s;
+}
+
+// one wave: walk tile clusters [cfrom, nact) for the row with metadata m (encoding offset,
+// #blocks, SC, S1C) and first encoding chunk pre (entries l + 64u, 0 past the row) with the
+// estimate; returns EV_ACCEPT | c, EV_EXACT | c (guard band: the exact emulation must decide c)
+// or EV_REJECT. Estimate: fp32 products and minima (relative error <= 2 ulp each), summed in
+// fp32 over 4 entries and in double beyond: < 5e-7 relative in total, far inside GUARD.
+template <u32 TS>
+__device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl& C, uint4 m,
+                        const u32 (&pre)[4], u32 cfrom, u32 nact) {
+    const u32 l = lane_id();
+    const u32 b0 = m.x, nb = m.y, scr = m.z, s1c = m.w;
+    const float nc = sqrtf(static_cast<float>(scr));
+    const bool est = !a.exact_all && scr != 0;
+    double red = 0.0;
+    if (est) {
+        double mn[CL_TMAX];
+        float inr[TS];
+#pragma unroll
+        for (u32 c = 0; c < CL_TMAX; ++c) mn[c] = 0.0;
+#pragma unroll
+        for (u32 c = 0; c < TS; ++c) inr[c] = C.inrf[c];
+        const float incf = 1.0f / nc;
+        u32 ent[4] = {pre[0], pre[1], pre[2], pre[3]};
+        for (u32 e0 = l; e0 < nb; e0 += 256) {
+            if (e0 != l) {
+#pragma unroll
+                for (u32 u = 0; u < 4; ++u) {
+                    const u32 e = e0 + 64 * u;
+                    ent[u] = e < nb ? a.enc[b0 + e] : 0u;
+                }
+            }
+            float s[TS];
+#pragma unroll
+            for (u32 c = 0; c < TS; ++c) s[c] = 0.0f;
+#pragma unroll
+            for (u32 u = 0; u < 4; ++u) {
+                const u32 blk = ent[u] & 0xFFFFu;
+                // a padding or non-kept entry contributes min(x, 0) = 0
+                const float y = (ent[u] && kept_idx(blk, a.B, a.keptMask))
+                                    ? static_cast<float>(ent[u] >> 16) * incf
+                                    : 0.0f;
+                const u32* rp = reps + blk * TS;
+                u32 rv[TS];
+                if constexpr (TS % 4 == 0) {
+#pragma unroll
+                    for (u32 q = 0; q < TS; q += 4) {
+                        const uint4 v4 = *reinterpret_cast<const uint4*>(rp + q);
+                        rv[q] = v4.x;
+                        rv[q + 1] = v4.y;
+                        rv[q + 2] = v4.z;
+                        rv[q + 3] = v4.w;
+                    }
+                } else {
+#pragma unroll
+                    for (u32 q = 0; q < TS; q += 2) {
+                        const uint2 v2 = *reinterpret_cast<const uint2*>(rp + q);
+                        rv[q] = v2.x;
+                        rv[q + 1] = v2.y;
+                    }
+                }
+#pragma unroll
+                for (u32 c = 0; c < TS; ++c)
+                    s[c] += fminf(static_cast<float>(rv[c]) * inr[c], y);
+            }
+#pragma unroll
+            for (u32 c = 0; c < TS; ++c) mn[c] += static_cast<double>(s[c]);
+        }
+        red = wave_sum8(mn);
+    }
+    for (u32 c = cfrom; c < nact; ++c) {
+        const u32 SR = C.SR[c];
+        if (SR == 0 && scr == 0) {
+            if (1.0f > a.alpha) return EV_ACCEPT | c;
+            continue;
+        }
+        if (SR == 0 || scr == 0) {
+            if (0.0f > a.alpha) return EV_ACCEPT | c;
+            continue;
+        }
+        if (!est) return EV_EXACT | c;
+        const double mnc = readlane_f64(red, 8 * c);
+        const double mx = static_cast<double>(C.S1R[c]) / C.nr[c] + static_cast<double>(s1c) / nc - mnc;
+        const double sim = mnc / mx;
+        const double ad = static_cast<double>(a.alpha);
+        if (fabs(sim - ad) > GUARD) {
+            if (sim > ad) return EV_ACCEPT | c;
+            continue;
+        }
+        return EV_EXACT | c;
+    }
+    return EV_REJECT;
+}
+
+__device__ __forceinline__ void load_chunk0(const ClusterArgs& a, uint4 m, u32 (&ent)[4]) {
+    const u32 l = lane_id();
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u) {
+        const u32 e = l + 64 * u;
+        ent[u] = e < m.y ? a.enc[m.x + e] : 0u;
+    }
+}
+
+template <u32 TS>
+__global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) u32 smem[];
+    constexpr u32 T = TS;
+    u32* reps = smem;  // [NP][TS]: block b of tile cluster c at reps[b * TS + c]
+    ClusterCtl& C = *reinterpret_cast<ClusterCtl*>(smem + a.NP * TS);
+    const u32 tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+    __shared__ u32 s_ticket;
+    if (tid == 0) s_ticket = atomicAdd(&a.ctrl[6], 1u);
+    for (u32 x = tid; x < a.NP * TS; x += blockDim.x) reps[x] = 0;
+    if (tid < CL_TMAX) {
+        C.inrf[tid] = 0.0f;
+        C.nr[tid] = 0.0f;
+        C.SR[tid] = 0;
+        C.S1R[tid] = 0;
+    }
+    __syncthreads();
+    const u32 ticket = s_ticket;
+    const u32 kfirst = a.c0 + ticket * T, klast = kfirst + T - 1, pred = kfirst - 1;
     u32* cmp = a.cmpScratch + static_cast<size_t>(ticket) * a.nbpr;  // zero between uses
     const u32 M = a.M;
-    u64 nexact = 0, ntotal = 0;
-    bool aborted = false;
 
     auto check_abort = [&](u64 t_start) -> bool {
         u32 ab = 0;
@@ -243,216 +416,261 @@ __global__ __launch_bounds__(64) void k_cluster(ClusterArgs a) {
         }
         return __shfl(ab, 0) != 0;
     };
+    auto set_norm = [&](u32 c, u32 sr) {  // lane 0
+        C.SR[c] = sr;
+        const float nr = sqrtf(static_cast<float>(sr));
+        C.nr[c] = nr;
+        C.inrf[c] = sr ? 1.0f / nr : 0.0f;
+    };
+    // leader: start a new tile cluster (index C.nact) at position p (metadata m)
+    auto new_cluster = [&](u32 p, uint4 m) {
+        const u32 c = C.nact;
+        for (u32 e = l; e < m.y; e += 64) {
+            const u32 ent = a.enc[m.x + e];
+            reps[(ent & 0xFFFFu) * TS + c] = ent >> 16;
+        }
+        if (l == 0) {
+            set_norm(c, m.z);
+            C.S1R[c] = m.w;
+            C.nact = c + 1;
+            st_agent(&a.state[p], ASSIGNED | (kfirst + c));
+            st_agent(&a.st[kfirst + c], p + 2);
+        }
+    };
+    // leader: position p (metadata m) joins tile cluster c
+    auto accept = [&](u32 p, uint4 m, u32 c) {
+        u32 dsr = 0, ds1 = 0;
+        for (u32 e = l; e < m.y; e += 64) {
+            const u32 ent = a.enc[m.x + e];
+            const u32 blk = ent & 0xFFFFu, cnt = ent >> 16;
+            const u32 o = reps[blk * TS + c], nv = o + cnt;
+            reps[blk * TS + c] = nv;
+            if (kept_idx(blk, a.B, a.keptMask)) {
+                dsr += nv * nv - o * o;
+                ds1 += cnt;
+            }
+        }
+        dsr = wave_sum(dsr);
+        ds1 = wave_sum(ds1);
+        if (l == 0) {
+            set_norm(c, C.SR[c] + dsr);
+            C.S1R[c] += ds1;
+            st_agent(&a.state[p], ASSIGNED | (kfirst + c));
+        }
+    };
+    // leader: exact similarity of tile cluster c with the row of metadata m
+    auto exact = [&](uint4 m, u32 c) -> bool {
+        for (u32 e = l; e < m.y; e += 64) {
+            const u32 ent = a.enc[m.x + e];
+            cmp[ent & 0xFFFFu] = ent >> 16;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const float nc = sqrtf(static_cast<float>(m.z));
+        const float sim = sim_exact_wave<TS>(reps + c, cmp, a.nbpr, a.B, C.nr[c], nc);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        for (u32 e = l; e < m.y; e += 64) cmp[a.enc[m.x + e] & 0xFFFFu] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        return sim > a.alpha;
+    };
+    auto row_meta = [&](u32 p) -> uint4 {
+        const u32 row = a.asc[p];
+        return make_uint4(a.rowptr[row], a.nblk[row], a.SC[row], a.S1C[row]);
+    };
 
-    // ---- wait for the predecessor's start
-    u32 sprev = 0;
-    {
-        const u64 t0 = now_ticks();
+    // ---- leader: wait for the predecessor tile's last start, find the first cluster's start
+    if (w == 0) {
+        u32 start = M;
+        bool aborted = false;
+        u32 sprev = 0;
+        u64 t0 = now_ticks();
         while (true) {
             u32 v = 0;
-            if (l == 0) v = ld_agent(&a.st[k - 1]);
+            if (l == 0) v = ld_agent(&a.st[pred]);
             v = __shfl(v, 0);
             if (v != 0) {
                 sprev = v;
                 break;
             }
-            if (check_abort(t0)) return;
-            __builtin_amdgcn_s_sleep(4);
-        }
-    }
-    if (sprev == ST_NONE) {
-        if (l == 0) st_agent(&a.st[k], ST_NONE);
-        return;
-    }
-    const u32 pred = k - 1;
-
-    // ---- find the start: first position after the predecessor's start rejected by it
-    u32 i = sprev - 1;
-    u32 start = M;
-    {
-        u64 t0 = now_ticks();
-        while (i < M) {
-            const u32 idx = i + l;
-            const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
-            const bool ready = (v & ASSIGNED) || v == pred;
-            const u64 notready = __ballot(!ready);
-            const u32 L = notready ? __builtin_ctzll(notready) : 64u;
-            const u64 cand = __ballot(ready && !(v & ASSIGNED) && l < L);
-            if (cand) {
-                start = i + __builtin_ctzll(cand);
-                break;
-            }
-            if (L == 0) {
-                if (check_abort(t0)) {
-                    aborted = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            } else {
-                i += L;
-                t0 = now_ticks();
-            }
-        }
-    }
-    if (aborted) return;
-    if (start >= M) {
-        if (l == 0) st_agent(&a.st[k], ST_NONE);
-        return;
-    }
-    if (l == 0) {
-        st_agent(&a.state[start], ASSIGNED | k);
-        st_agent(&a.st[k], start + 2);
-    }
-    // representative = encoding of the start row
-    for (u32 x = l; x < a.nbpr; x += 64) rep[x] = 0;
-    __syncthreads();
-    u32 SR, SC0;
-    u64 S1R;
-    {
-        const u32 row = a.asc[start];
-        const u32 b0 = a.rowptr[row], nb = a.nblk[row];
-        for (u32 e = l; e < nb; e += 64) {
-            const u32 ent = a.enc[b0 + e];
-            rep[ent & 0xFFFFu] = ent >> 16;
-        }
-        SR = a.SC[row];
-        S1R = a.S1C[row];
-        (void)SC0;
-    }
-    __syncthreads();
-
-    // ---- main loop
-    i = start + 1;
-    u64 t0 = now_ticks();
-    while (i < M) {
-        const u32 idx = i + l;
-        const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
-        const bool ready = (v & ASSIGNED) || v == pred;
-        const u64 notready = __ballot(!ready);
-        const u32 L = notready ? __builtin_ctzll(notready) : 64u;
-        if (L == 0) {
             if (check_abort(t0)) {
                 aborted = true;
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
+            __builtin_amdgcn_s_sleep(4);
         }
-        const bool mine = !(v & ASSIGNED) && l < L;
-        u64 todo = __ballot(mine);
-        // the batch's row metadata in one round trip (lane j: position i + j), and each
-        // position's first 64 encoding entries loaded while the previous position computes; the
-        // representative (LDS) is the only state an accept changes, so the loads are order-free
-        u32 m_b0 = 0, m_nb = 0, m_sc = 0, m_s1 = 0;
-        if (mine) {
-            const u32 row = a.asc[idx];
-            m_b0 = a.rowptr[row];
-            m_nb = a.nblk[row];
-            m_sc = a.SC[row];
-            m_s1 = a.S1C[row];
-        }
-        u32 ent0 = 0;
-        if (todo) {
-            const u32 jn = __builtin_ctzll(todo);
-            const u32 nb0 = __shfl(m_b0, jn), nnb = __shfl(m_nb, jn);
-            ent0 = l < nnb ? a.enc[nb0 + l] : 0u;
-        }
-        while (todo) {
-            const u32 j = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const u32 pos = i + j;
-            const u32 b0 = __shfl(m_b0, j), nb = __shfl(m_nb, j);
-            const u32 SCr = __shfl(m_sc, j);
-            const u32 S1Cr = __shfl(m_s1, j);
-            const u32 cur0 = ent0;  // enc[b0 + l] (l < nb)
-            if (todo) {
-                const u32 jn = __builtin_ctzll(todo);
-                const u32 nb0 = __shfl(m_b0, jn), nnb = __shfl(m_nb, jn);
-                ent0 = l < nnb ? a.enc[nb0 + l] : 0u;
-            }
-            ++ntotal;
-            bool accept;
-            if (SR == 0 && SCr == 0) {
-                accept = 1.0f > a.alpha;
-            } else if (SR == 0 || SCr == 0) {
-                accept = 0.0f > a.alpha;
-            } else {
-                const float nr = sqrtf(static_cast<float>(SR));
-                const float nc = sqrtf(static_cast<float>(SCr));
-                bool decided = false;
-                accept = false;
-                if (!a.exact_all) {
-                    // the estimate only has to land outside the guard band: reciprocals (1e-16
-                    // relative) instead of two f64 divisions per block, four encoding loads in
-                    // flight per lane
-                    const double inr = 1.0 / static_cast<double>(nr);
-                    const double inc = 1.0 / static_cast<double>(nc);
-                    double mn = 0.0;
-                    for (u32 e0 = l; e0 < nb; e0 += 256) {
-                        u32 ent[4];
-#pragma unroll
-                        for (u32 u = 0; u < 4; ++u) {
-                            const u32 e = e0 + 64 * u;
-                            ent[u] = e < nb ? (e < 64 ? cur0 : a.enc[b0 + e]) : 0u;
-                        }
-#pragma unroll
-                        for (u32 u = 0; u < 4; ++u) {
-                            const u32 blk = ent[u] & 0xFFFFu;
-                            const u32 rv = rep[blk];
-                            if (e0 + 64 * u < nb && rv && kept_idx(blk, a.B, a.keptMask))
-                                mn += fmin(static_cast<double>(rv) * inr,
-                                           static_cast<double>(ent[u] >> 16) * inc);
-                        }
-                    }
-                    mn = wave_sum(mn);
-                    const double mx = static_cast<double>(S1R) / nr +
-                                      static_cast<double>(S1Cr) / nc - mn;
-                    const double sim = mn / mx;
-                    const double ad = static_cast<double>(a.alpha);
-                    if (fabs(sim - ad) > GUARD) {
-                        decided = true;
-                        accept = sim > ad;
-                    }
+        if (!aborted && sprev != ST_NONE) {
+            u32 i = sprev - 1;
+            t0 = now_ticks();
+            while (i < M) {
+                const u32 idx = i + l;
+                const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
+                const bool ready = (v & ASSIGNED) || v == pred;
+                const u64 notready = __ballot(!ready);
+                const u32 L = notready ? __builtin_ctzll(notready) : 64u;
+                const u64 cand = __ballot(ready && !(v & ASSIGNED) && l < L);
+                if (cand) {
+                    start = i + __builtin_ctzll(cand);
+                    break;
                 }
-                if (!decided) {
-                    ++nexact;
-                    for (u32 e = l; e < nb; e += 64) {
-                        const u32 ent = a.enc[b0 + e];
-                        cmp[ent & 0xFFFFu] = ent >> 16;
+                if (L == 0) {
+                    if (check_abort(t0)) {
+                        aborted = true;
+                        break;
                     }
-                    __syncthreads();
-                    const float sim = sim_exact(rep, cmp, a.nbpr, a.B, a.keptMask, nr, nc, smn, smx);
-                    accept = sim > a.alpha;
-                    for (u32 e = l; e < nb; e += 64) cmp[a.enc[b0 + e] & 0xFFFFu] = 0;
-                    __syncthreads();
+                    __builtin_amdgcn_s_sleep(2);
+                } else {
+                    i += L;
+                    t0 = now_ticks();
                 }
             }
-            if (accept) {
-                u32 dsr = 0, ds1 = 0;
-                for (u32 e = l; e < nb; e += 64) {
-                    const u32 ent = e < 64 ? cur0 : a.enc[b0 + e];
-                    const u32 blk = ent & 0xFFFFu, c = ent >> 16;
-                    const u32 o = rep[blk], nv = o + c;
-                    rep[blk] = nv;
-                    if (kept_idx(blk, a.B, a.keptMask)) {
-                        dsr += nv * nv - o * o;
-                        ds1 += c;
-                    }
-                }
-                SR += wave_sum(dsr);
-                S1R += wave_sum(ds1);
-                __syncthreads();
-            }
-            if (l == 0) st_agent(&a.state[pos], accept ? (ASSIGNED | k) : k);
         }
-        i += L;
-        t0 = now_ticks();
+        if (l == 0) {
+            C.nact = 0;
+            C.nexact = 0;
+            C.ntotal = 0;
+            C.done = (aborted || start >= M) ? 1u : 0u;
+            C.i = start + 1;
+        }
+        if (!aborted && start < M) {
+            const uint4 m = row_meta(start);
+            new_cluster(start, m);
+        }
+        if (aborted && l == 0) C.nact = T;  // no ST_NONE on abort: the host reports the timeout
     }
-    (void)aborted;
-    (void)s_abort;
-    if (l == 0) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[2]), nexact);
-        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[4]), ntotal);
+    __syncthreads();
+
+    u64 t_idle = now_ticks();
+    while (!C.done) {
+        __syncthreads();  // every wave has read the previous window's control words
+        // ---- leader: next window of ready positions (rejected by the predecessor tile or
+        // assigned); the unassigned ones and their rows' metadata go to C.todo / C.meta
+        if (w == 0) {
+            u32 i = C.i, n = 0, total = 0;
+            bool stop = false;
+            while (!stop && total < CL_WIN && i + total < M) {
+                const u32 idx = i + total + l;
+                const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
+                const bool ready = (v & ASSIGNED) || v == pred;
+                const u64 notready = __ballot(!ready || idx >= M);
+                const u32 L = notready ? __builtin_ctzll(notready) : 64u;
+                const bool mine = !(v & ASSIGNED) && l < L;
+                const u64 mm = __ballot(mine);
+                if (mine) {
+                    const u32 slot = n + __builtin_amdgcn_mbcnt_hi(
+                                             static_cast<u32>(mm >> 32),
+                                             __builtin_amdgcn_mbcnt_lo(static_cast<u32>(mm), 0u));
+                    C.todo[slot] = idx;
+                    C.meta[slot] = row_meta(idx);
+                }
+                n += __builtin_popcountll(mm);
+                total += L;
+                stop = L < 64;
+            }
+            bool aborted = false;
+            if (total == 0 && i < M) {
+                if (check_abort(t_idle)) aborted = true;
+                else __builtin_amdgcn_s_sleep(1);
+            } else {
+                t_idle = now_ticks();
+            }
+            if (l == 0) {
+                C.ntodo = n;
+                C.t = 0;
+                C.i = i + total;
+                if (aborted) {
+                    C.done = 1;
+                    C.nact = T;
+                }
+                if (i + total >= M && n == 0) C.done = 1;
+            }
+        }
+        __syncthreads();
+        if (C.done && C.ntodo == 0) break;
+        // ---- evaluate / resolve sub-batches
+        while (true) {
+            const u32 t = C.t, ntodo = C.ntodo, nact = C.nact;
+            if (t >= ntodo) break;
+            const u32 tend = min(ntodo, t + CL_SUB);
+            {
+                u32 j = t + w;
+                u32 pre[4];
+                uint4 m = make_uint4(0, 0, 0, 0);
+                if (j < tend) {
+                    m = C.meta[j];
+                    load_chunk0(a, m, pre);
+                }
+                while (j < tend) {
+                    const u32 jn = j + CL_WAVES;
+                    const u32 cur[4] = {pre[0], pre[1], pre[2], pre[3]};
+                    const uint4 mc = m;
+                    if (jn < tend) {  // the next row's first chunk in flight while this one runs
+                        m = C.meta[jn];
+                        load_chunk0(a, m, pre);
+                    }
+                    const u32 r = eval_row<TS>(a, reps, C, mc, cur, 0, nact);
+                    if (l == 0) C.res[j] = r;
+                    j = jn;
+                }
+            }
+            __syncthreads();
+            if (w == 0) {
+                u32 j = t;
+                u64 nex = 0, ntot = 0;
+                while (j < tend) {
+                    // plain rejects of a full tile up to the first event, stored lane-parallel
+                    const u32 n = tend - j;
+                    const u32 r = l < n ? C.res[j + l] : EV_REJECT;
+                    const u64 ev = __ballot(l < n && (r != EV_REJECT || C.nact < T));
+                    const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : n;
+                    if (l < e) st_agent(&a.state[C.todo[j + l]], klast);
+                    ntot += static_cast<u64>(e) * C.nact;
+                    j += e;
+                    if (j >= tend) break;
+                    // the event: exact emulation where the estimate is in the guard band, then
+                    // an accept or a new cluster; the positions after it are evaluated again
+                    const u32 p = C.todo[j];
+                    const uint4 m = C.meta[j];
+                    u32 rr = C.res[j];
+                    while ((rr & EV_EXACT) != 0) {
+                        const u32 c = rr & 0xFFu;
+                        ++nex;
+                        if (exact(m, c)) {
+                            rr = EV_ACCEPT | c;
+                        } else if (c + 1 < C.nact) {
+                            u32 pre[4];
+                            load_chunk0(a, m, pre);
+                            rr = eval_row<TS>(a, reps, C, m, pre, c + 1, C.nact);
+                        } else {
+                            rr = EV_REJECT;
+                        }
+                    }
+                    ++j;
+                    if (rr & EV_ACCEPT) {
+                        const u32 c = rr & 0xFFu;
+                        ntot += c + 1;
+                        accept(p, m, c);
+                        break;
+                    }
+                    ntot += C.nact;
+                    if (C.nact < T) {
+                        new_cluster(p, m);
+                        break;
+                    }
+                    if (l == 0) st_agent(&a.state[p], klast);
+                }
+                if (l == 0) {
+                    C.t = j;
+                    C.nexact += nex;
+                    C.ntotal += ntot;
+                }
+            }
+            __syncthreads();
+        }
+        if (C.done) break;
+    }
+    if (w == 0 && l == 0) {
+        for (u32 c = C.nact; c < T; ++c) st_agent(&a.st[kfirst + c], ST_NONE);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[2]), C.nexact);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[4]), C.ntotal);
     }
 }
 
@@ -1457,9 +1675,9 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     // 3. clustering
     DevBuf<u32> state, st, ctrl;
     BSMR_CHECK(state.alloc(M));
-    BSMR_CHECK(st.alloc(M + 2ull));
+    BSMR_CHECK(st.alloc(M + 2ull + CL_TMAX));  // the last tile may name up to T - 1 ids past M
     BSMR_CHECK(ctrl.alloc(8));
-    BSMR_HIP(hipMemsetAsync(st.data(), 0, (M + 2ull) * sizeof(u32), s));
+    BSMR_HIP(hipMemsetAsync(st.data(), 0, (M + 2ull + CL_TMAX) * sizeof(u32), s));
     BSMR_HIP(hipMemsetAsync(ctrl.data(), 0, 8 * sizeof(u32), s));
     hipLaunchKernelGGL(k_init_state, dim3(grid_for(M, 256)), dim3(256), 0, s, state.data(), st.data(),
                        M, z);
@@ -1481,24 +1699,37 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     ca.alpha = alpha;
     ca.exact_all = exact_all;
     ca.timeout_ticks = 100ull * 1000 * 1000 * 20;  // 20 s without progress
-    const size_t lds_cl = (((nbpr + 3) & ~3u) + 64) * sizeof(u32);
-    // clusters per launch: each workgroup takes the next cluster id from a ticket counter and
-    // waits only for its predecessor, which therefore has always started, so more clusters than
-    // fit on the chip at once cannot deadlock (later ones start as earlier ones finish); capped by
-    // the exact path's scratch (<= 256 MiB)
-    const u32 Rmax = static_cast<u32>(std::max<u64>(
-        64, std::min<u64>(cluster_batch, (64ull << 20) / std::max<u32>(nbpr, 1))));
+    // tile of T clusters: as many representatives as fit the LDS budget, at most CL_TMAX, an
+    // even number (block b of cluster c at reps[b * T + c]: 8- or 16-byte LDS reads of all T)
+    const u32 NP = (nbpr + 3) & ~3u;
+    const u32 T = std::max<u32>(2, std::min<u32>(CL_TMAX, CL_LDS_BUDGET / (NP * 4)) & ~1u);
+    ca.NP = NP;
+    ca.T = T;
+    const size_t lds_cl = static_cast<size_t>(T) * NP * 4 + sizeof(ClusterCtl);
+    // clusters per launch (a multiple of T): each tile takes the next T cluster ids from a
+    // ticket counter and waits only for its predecessor tile, which therefore has always started,
+    // so more tiles than fit on the chip at once cannot deadlock (later ones start as earlier
+    // ones finish); capped by the exact path's scratch (<= 256 MiB)
+    const u32 Rcap = static_cast<u32>(std::max<u64>(
+        T, std::min<u64>(cluster_batch, (64ull << 20) / std::max<u32>(nbpr, 1)) / T * T));
+    const u32 tilesMax = Rcap / T;
     DevBuf<u32> cmpScratch;
-    BSMR_CHECK(cmpScratch.alloc(static_cast<size_t>(Rmax) * nbpr));
-    BSMR_HIP(hipMemsetAsync(cmpScratch.data(), 0, static_cast<size_t>(Rmax) * nbpr * sizeof(u32), s));
+    BSMR_CHECK(cmpScratch.alloc(static_cast<size_t>(tilesMax) * nbpr));
+    BSMR_HIP(hipMemsetAsync(cmpScratch.data(), 0, static_cast<size_t>(tilesMax) * nbpr * sizeof(u32), s));
     ca.cmpScratch = cmpScratch.data();
     u32 c0 = 1;
     u32 last_valid = 0;
     while (c0 <= M) {  // at most M - z clusters
-        const u32 R = std::min<u32>(Rmax, M + 1 - c0);
+        const u32 tiles = std::min<u32>(tilesMax, (M + 1 - c0 + T - 1) / T);
+        const u32 R = tiles * T;
         ca.c0 = c0;
         BSMR_HIP(hipMemsetAsync(ctrl.data() + 6, 0, sizeof(u32), s));  // ticket counter
-        hipLaunchKernelGGL(k_cluster, dim3(R), dim3(64), lds_cl, s, ca);
+        switch (T) {
+            case 2: hipLaunchKernelGGL(k_cluster<2>, dim3(tiles), dim3(64 * CL_WAVES), lds_cl, s, ca); break;
+            case 4: hipLaunchKernelGGL(k_cluster<4>, dim3(tiles), dim3(64 * CL_WAVES), lds_cl, s, ca); break;
+            case 6: hipLaunchKernelGGL(k_cluster<6>, dim3(tiles), dim3(64 * CL_WAVES), lds_cl, s, ca); break;
+            default: hipLaunchKernelGGL(k_cluster<8>, dim3(tiles), dim3(64 * CL_WAVES), lds_cl, s, ca); break;
+        }
         BSMR_HIP(hipGetLastError());
         std::vector<u32> hst(R);
         BSMR_HIP(hipMemcpyAsync(hst.data(), st.data() + c0, R * sizeof(u32), hipMemcpyDeviceToHost, s));
