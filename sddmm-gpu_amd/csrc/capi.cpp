@@ -62,6 +62,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         p.orig_rows = orr[0] == '0' ? 0 : orr[0] == '1' ? 1 : -1;
     if (const char* oc = std::getenv("BSMR_ORIG_CONTIG")) p.orig_contig = std::atoi(oc);
     if (const char* dk = std::getenv("BSMR_DENSE_KS")) p.dense_ks = std::atoi(dk);
+    if (const char* dn = std::getenv("BSMR_DENSE_NS")) p.dense_ns = std::atoi(dn);
     if (const char* os = std::getenv("BSMR_OUT_STAGED"))  // "0" never, "1" always, else auto
         p.out_staged = os[0] == '0' ? 0 : os[0] == '1' ? 1 : -1;
     if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB")) {

@@ -199,6 +199,7 @@ struct Plan {
     };
     mutable DenseLayout dense;
     int dense_ks = 0;  // BSMR_DENSE_KS: 1 / 2 wave sets per tile, else by tile count
+    int dense_ns = 2;  // BSMR_DENSE_NS: LDS stages of the split-k dense launch (2..5)
     int build_dense_layout() const;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);

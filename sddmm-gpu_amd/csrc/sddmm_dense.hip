@@ -40,6 +40,8 @@ struct DenseArgs {
     const u32* out;  // CSR position
     u32 M, N, K, ntn, ntiles;
     unsigned long long bA, bB, bP;  // batched launch: A/B byte strides, P element stride
+    unsigned long long* trace;      // BSMR_DIAG & 32: per workgroup {start, chunk 0 landed,
+                                    // end, xcc << 60 | k-loop end} (s_memrealtime); else null
 };
 
 // 16-byte slot of (row r, k-group g) in a chunk image of KC/8 groups per row: the groups of a
@@ -95,27 +97,29 @@ __device__ __forceinline__ f32x4 mfma16x16x32(const f32x4 x, const f32x4 y, cons
                                                        __builtin_bit_cast(b16x8, y), c, 0, 0, 0);
 }
 
-// k-steps kset, kset + KS, ... of one k-chunk of the wave's 64 x 64 quadrant from the images
-// (sa, sb)
-template <int DT, u32 KC, u32 KS>
+// one k-chunk of the wave's 64 x (16 NJ) block of the tile from the images (sa, sb): rows
+// [64 wy, +64) of A, rows [16 NJ wx, +16 NJ) of B, every k-step
+template <int DT, u32 KC, u32 NJ>
 __device__ __forceinline__ void dense_chunk(const char* sa, const char* sb, const u32 wy,
-                                            const u32 wx, const u32 lane, const u32 kset,
-                                            f32x4 (&acc)[4][4]) {
+                                            const u32 wx, const u32 lane, f32x4 (&acc)[4][NJ]) {
     const u32 rr = lane & 15, g4 = lane >> 4;
 #pragma unroll
-    for (u32 k0 = 0; k0 < KC / 32; k0 += KS) {
-        const u32 ks = k0 + kset;
-        f32x4 av[4], bv[4];
+    for (u32 ks = 0; ks < KC / 32; ++ks) {
+        f32x4 av[4], bv[NJ];
 #pragma unroll
         for (u32 i = 0; i < 4; ++i) {
-            const u32 ra = 64 * wy + 16 * i + rr, rb = 64 * wx + 16 * i + rr;
+            const u32 ra = 64 * wy + 16 * i + rr;
             av[i] = *reinterpret_cast<const f32x4*>(sa + 16 * dslot<KC>(ra, 4 * ks + g4));
-            bv[i] = *reinterpret_cast<const f32x4*>(sb + 16 * dslot<KC>(rb, 4 * ks + g4));
+        }
+#pragma unroll
+        for (u32 j = 0; j < NJ; ++j) {
+            const u32 rb = 16 * NJ * wx + 16 * j + rr;
+            bv[j] = *reinterpret_cast<const f32x4*>(sb + 16 * dslot<KC>(rb, 4 * ks + g4));
         }
 #pragma unroll
         for (u32 i = 0; i < 4; ++i)
 #pragma unroll
-            for (u32 jj = 0; jj < 4; ++jj) acc[i][jj] = mfma16x16x32<DT>(av[i], bv[jj], acc[i][jj]);
+            for (u32 j = 0; j < NJ; ++j) acc[i][j] = mfma16x16x32<DT>(av[i], bv[j], acc[i][j]);
     }
 }
 
@@ -125,19 +129,16 @@ constexpr u32 dense_lds() { return NS * 2 * chunk_bytes<KC>(); }
 template <u32 KC, u32 NS>
 constexpr u32 dense_wgs() { return 160u * 1024 / dense_lds<KC, NS>() < 4 ? 160u * 1024 / dense_lds<KC, NS>() : 4; }
 
-// KS = 1: four waves, one 64 x 64 quadrant each. KS = 2: eight waves, waves 4..7 take the odd
-// k-steps of every chunk on the same quadrants (two waves per SIMD, so one wave's LDS reads run
-// under the other's MFMAs when the tiles give one workgroup per CU); partial tiles summed in LDS
-template <int DT, u32 KC, u32 NS, u32 KS>
-__global__ __launch_bounds__(256 * KS)
-__attribute__((amdgpu_waves_per_eu(dense_wgs<KC, NS>() * KS < 4 ? dense_wgs<KC, NS>() * KS : 4)))
+// NW = 4: four waves, a 64 x 64 quadrant each. NW = 8: eight waves, a 64 x 32 block each (two
+// waves per SIMD, so one wave's LDS reads run under the other's MFMAs when the tiles give one
+// workgroup per CU)
+template <int DT, u32 KC, u32 NS, u32 NW>
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu(dense_wgs<KC, NS>() * NW / 4 < 4 ? dense_wgs<KC, NS>() * NW / 4 : 4)))
 void k_sddmm_dense(DenseArgs a) {
-    constexpr u32 NT = 256 * KS, NWAV = 4 * KS, ND = dense_nd<KC, NWAV>();
+    constexpr u32 NT = 64 * NW, ND = dense_nd<KC, NW>(), NJ = 16 / NW;
     constexpr u32 CB = chunk_bytes<KC>(), LDS = dense_lds<KC, NS>();
-    // NS stages of (A chunk, B chunk) images; the finished fp32 tile passes through the same
-    // bytes, CR rows (of 512 bytes) at a time
-    constexpr u32 CR = LDS >= DT_TILE * 512 ? DT_TILE : 64;  // passes of whole wave rows
-    static_assert(LDS >= CR * 512, "the epilogue pass fits the stage images");
+    static_assert(LDS >= DT_TILE * DT_TILE * 4, "the fp32 tile fits the stage images");
     __shared__ __attribute__((aligned(16))) char st[LDS];
     if (blockIdx.y) {
         a.A += blockIdx.y * a.bA;
@@ -153,63 +154,91 @@ void k_sddmm_dense(DenseArgs a) {
     const u32 tm = t / a.ntn, tn = t - tm * a.ntn;
     const u32 r0 = DT_TILE * tm, c0 = DT_TILE * tn;
     const u32 tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const u32 ws = __builtin_amdgcn_readfirstlane(w), kset = ws >> 2, wy = (ws >> 1) & 1, wx = ws & 1;
-    static_assert(KS == 1 || (KS == 2 && KC / 32 == 2), "one k-step per wave set and chunk");
-    f32x4 acc[4][4];
+    const u32 ws = __builtin_amdgcn_readfirstlane(w);
+    const u32 wy = NW == 4 ? ws >> 1 : ws >> 2, wx = NW == 4 ? ws & 1 : ws & 3;
+    f32x4 acc[4][NJ];
 #pragma unroll
     for (u32 i = 0; i < 4; ++i)
 #pragma unroll
-        for (u32 jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (u32 jj = 0; jj < NJ; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long t_first = 0;
     const u32 nk = a.K / KC;  // launch_dense: K a multiple of KC
     // chunk kc lands in stage kc % NS. Before a stage is read every wave waits for its own
-    // LDS-DMAs into it (KC/8 per stage; those of the NS - 2 younger stages may stay in flight)
-    // and the workgroup barrier then makes everyone's visible; the same barrier ends all reads
-    // of the stage the next prefetch overwrites. Prefetches past the last chunk re-read it (no
-    // branch around an LDS-DMA).
+    // LDS-DMAs into it (2 ND per chunk; those of the younger chunks already issued may stay in
+    // flight) and the workgroup barrier then makes everyone's visible; the same barrier ends all
+    // reads of the stage the next prefetch overwrites. No chunk past the last is staged.
     auto stage = [&](const u32 kc) {
         char* const sa = st + (kc % NS) * (2 * CB);
-        dense_stage<KC, NWAV>(a, r0, c0, min(kc, nk - 1), ws, lane, sa, sa + CB);
+        dense_stage<KC, NW>(a, r0, c0, kc, ws, lane, sa, sa + CB);
     };
 #pragma unroll
-    for (u32 j = 0; j + 1 < NS; ++j) stage(j);
+    for (u32 j = 0; j + 1 < NS; ++j)
+        if (j < nk) stage(j);
     for (u32 kc = 0; kc < nk; ++kc) {
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * ND * (NS - 2)) : "memory");
-        stage(kc + NS - 1);
+        if (NS > 2 && kc + NS - 2 < nk)
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * ND * (NS > 2 ? NS - 2 : 0)) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (a.trace && kc == 0) t_first = __builtin_amdgcn_s_memrealtime();
+        if (kc + NS - 1 < nk) stage(kc + NS - 1);
         const char* const sa = st + (kc % NS) * (2 * CB);
-        dense_chunk<DT, KC, KS>(sa, sa + CB, wy, wx, lane, kset, acc);
+        dense_chunk<DT, KC, NJ>(sa, sa + CB, wy, wx, lane, acc);
     }
-    // every read done, every LDS-DMA (the clamped tail prefetches too) landed: the images
-    // become the fp32 tile
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    // the first PF entries of each thread's share of the tile's stored entries (local offset,
+    // CSR position), loaded right after the k-loop (after every LDS-DMA, so no chunk wait
+    // includes them): their latency runs under the tile's LDS pass instead of after it
+    constexpr u32 PF = 4;
+    u32 pl[PF], po[PF];
+#pragma unroll
+    for (u32 q = 0; q < PF; ++q) {  // unconditional (clamped) loads: all 2 PF in flight at once
+        const u32 e = e0 + tid + NT * q, ec = min(e, e1 - 1);
+        const u32 lv = a.loc[ec], ov = a.out[ec];
+        pl[q] = e < e1 ? lv : NULLV;
+        po[q] = ov;
+    }
+    // every read of the images done (every LDS-DMA landed at the last chunk's wait): they
+    // become the fp32 tile, element (r, c) at ((r >> 2) * 128 + c) * 4 + (r & 3), so a lane's
+    // four accumulator rows are one 16-byte store
+    __syncthreads();
+    const unsigned long long t_loop = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     float* const ct = reinterpret_cast<float*>(st);
-    // accumulator (i, jj) reg r of lane l = D[64 wy + 16 i + 4 (l >> 4) + r][64 wx + 16 jj + (l & 15)];
-    // pass h holds tile rows [CR h, CR h + CR); KS = 2: wave set 1 stores its partial tile, set
-    // 0 adds its own
-    static_assert(KS == 1 || CR == DT_TILE, "split-k sums the whole tile in one pass");
+    // accumulator (i, jj) reg r of lane l = D[64 wy + 16 i + 4 (l >> 4) + r][16 NJ wx + 16 jj + (l & 15)]
 #pragma unroll
-    for (u32 h = 0; h < DT_TILE / CR; ++h) {
-        if (h) __syncthreads();  // the previous pass's reads are done
+    for (u32 i = 0; i < 4; ++i)
 #pragma unroll
-        for (u32 set = KS; set-- > 0;) {
-            if (set == kset && (CR == DT_TILE || wy == h)) {
-#pragma unroll
-                for (u32 i = 0; i < 4; ++i)
-#pragma unroll
-                    for (u32 jj = 0; jj < 4; ++jj)
-#pragma unroll
-                        for (u32 r = 0; r < 4; ++r) {
-                            float& c = ct[(64 * wy + 16 * i + 4 * (lane >> 4) + r - CR * h) * DT_TILE +
-                                          64 * wx + 16 * jj + (lane & 15)];
-                            c = set + 1 < KS ? c + acc[i][jj][r] : acc[i][jj][r];
-                        }
-            }
-            if (set) __syncthreads();  // the later set's stores land before the earlier adds
+        for (u32 jj = 0; jj < NJ; ++jj) {
+            const u32 rq = 16 * wy + 4 * i + (lane >> 4), col = 16 * NJ * wx + 16 * jj + (lane & 15);
+            *reinterpret_cast<f32x4*>(ct + (rq * DT_TILE + col) * 4) = acc[i][jj];
         }
-        __syncthreads();
-        for (u32 e = e0 + tid; e < e1; e += NT) {
-            const u32 lc = a.loc[e] - CR * DT_TILE * h;  // loc = local row * 128 + local column
-            if (lc < CR * DT_TILE) a.P[a.out[e]] = ct[lc];
+    __syncthreads();
+    auto at = [&](u32 lc) {  // loc = local row << 7 | local column
+        return ct[((lc >> 9) * DT_TILE + (lc & 127)) * 4 + ((lc >> 7) & 3)];
+    };
+#pragma unroll
+    for (u32 q = 0; q < PF; ++q)
+        if (pl[q] != NULLV) a.P[po[q]] = at(pl[q]);
+    // denser tiles: the rest PF entries at a time, loads unconditional so they overlap
+    for (u32 eb = e0 + tid + NT * PF; eb < e1; eb += NT * PF) {
+        u32 lv[PF], ov[PF];
+#pragma unroll
+        for (u32 q = 0; q < PF; ++q) {
+            const u32 ec = min(eb + NT * q, e1 - 1);
+            lv[q] = a.loc[ec];
+            ov[q] = a.out[ec];
         }
+#pragma unroll
+        for (u32 q = 0; q < PF; ++q)
+            if (eb + NT * q < e1) a.P[ov[q]] = at(lv[q]);
+    }
+    if (a.trace && tid == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        const u32 xcc = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+        unsigned long long* tr = a.trace + 4ull * (blockIdx.y * gridDim.x + blockIdx.x);
+        tr[0] = t_start;
+        tr[1] = t_first;
+        tr[2] = t_end;
+        tr[3] = (static_cast<unsigned long long>(xcc) << 60) | t_loop;
     }
 }
 
@@ -273,20 +302,39 @@ int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     const u32 per = (D.ntiles + XCD_BUCKETS - 1) / XCD_BUCKETS;
     const u32 grid = per * XCD_BUCKETS;
     const dim3 g(grid, nb);
+    a.trace = nullptr;
+    if (p.diag & 32) {
+        BSMR_CHECK(p.prepare_trace(static_cast<size_t>(grid) * nb, s));
+        a.trace = p.trace.data();
+    }
     // (KC, NS) = (64, 2): two workgroups per CU. Measured (tools/gpu_dense_stages.sh history,
     // r01q): 4 stages at one workgroup per CU and KC = 32 at 2-4 stages / 2-4 workgroups were
     // all slower (C5 uniform 10.6-12.1 us vs 8.8-9.8)
     // split-k wave sets when the tiles fill at most one workgroup per CU (C5: 256 tiles)
     const bool ks2 = p.dense_ks == 2 || (p.dense_ks != 1 && D.nonempty < 512);
     if (ks2) {
-        if (dtype == BSMR_F16)
-            hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2, 2>), g, dim3(512), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2, 2>), g, dim3(512), 0, s, a);
+        const bool f16 = dtype == BSMR_F16;
+        switch (p.dense_ns) {
+            case 3:
+                if (f16) hipLaunchKernelGGL((k_sddmm_dense<1, 64, 3, 8>), g, dim3(512), 0, s, a);
+                else hipLaunchKernelGGL((k_sddmm_dense<2, 64, 3, 8>), g, dim3(512), 0, s, a);
+                break;
+            case 4:
+                if (f16) hipLaunchKernelGGL((k_sddmm_dense<1, 64, 4, 8>), g, dim3(512), 0, s, a);
+                else hipLaunchKernelGGL((k_sddmm_dense<2, 64, 4, 8>), g, dim3(512), 0, s, a);
+                break;
+            case 5:
+                if (f16) hipLaunchKernelGGL((k_sddmm_dense<1, 64, 5, 8>), g, dim3(512), 0, s, a);
+                else hipLaunchKernelGGL((k_sddmm_dense<2, 64, 5, 8>), g, dim3(512), 0, s, a);
+                break;
+            default:
+                if (f16) hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2, 8>), g, dim3(512), 0, s, a);
+                else hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2, 8>), g, dim3(512), 0, s, a);
+        }
     } else if (dtype == BSMR_F16) {
-        hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2, 1>), g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_sddmm_dense<1, 64, 2, 4>), g, dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2, 1>), g, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_sddmm_dense<2, 64, 2, 4>), g, dim3(256), 0, s, a);
     }
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
     ap.add_argument("--waves-per-wg", type=int, default=16, help="NT / 64 of the traced launch")
+    ap.add_argument("--mask", default=None, help="dlmc_like mask: uniform | block")
     args = ap.parse_args()
     os.environ["BSMR_DIAG"] = str(int(os.environ.get("BSMR_DIAG", "0")) | 32)
     import torch
@@ -38,7 +39,10 @@ def main():
     from bsmr import Plan, make_data, synth
 
     gen = getattr(synth, args.workload)
-    M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
+    if args.mask is not None:
+        M, N, rp, ci = gen(args.mask)
+    else:
+        M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
     K = args.K
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout, lds_budget_kb=args.lds_kb)
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
