@@ -60,6 +60,11 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary with hbm_bytes_per_launch for roofline.traffic (default: "
                          "profiles/traffic_<config>_K<K>.json when present)")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
+                    help="roofline.traffic measured in this run: two rocprofv3 PMC passes "
+                         "(FETCH_SIZE, WRITE_SIZE) over tools/prof_sddmm.py on the same workload, "
+                         "run as child processes before this process touches the GPU (auto: at "
+                         "N=1 when rocprofv3 is on PATH)")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -261,13 +266,65 @@ def traffic_for(args, K):
                                            "status": "kernel sources match"}
 
 
+def pmc_traffic_inrun(args):
+    """roofline.traffic measured now: HBM bytes per launch of the fused SDDMM kernel on this
+    workload, from two rocprofv3 PMC passes (one counter each: FETCH_SIZE needs 3 of the 4 TCC
+    counters, WRITE_SIZE 2) over tools/prof_sddmm.py, corrected as MI355X_MICROARCH.md's HBM
+    section prescribes (FETCH_SIZE KiB x 2 on gfx950, WRITE_SIZE KiB as reported). The children
+    run before this process initialises the GPU. Returns (bytes or None, source dict)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    if args.pmc == "off":
+        return None, {"status": "--pmc off"}
+    rp = shutil.which("rocprofv3")
+    if not rp:
+        return None, {"status": "rocprofv3 not on PATH"}
+    wl = {"C2": ["--workload", "nips_like", "--dtype", "f32"],
+          "C3": ["--workload", "cop20k_like", "--dtype", "f16"],
+          "C4": ["--workload", "reddit_like", "--scale", str(args.scale), "--dtype", "f32"],
+          "C5": ["--workload", "dlmc_like", "--mask", args.mask, "--dtype", "bf16"]}[args.config]
+    K = args.K or {"C2": 128, "C3": 256, "C4": 128, "C5": 512}[args.config]
+    wl += ["--K", str(K), "--layout", args.layout, "--iters", "5"]
+    tmp = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
+    limit = 600 if args.config == "C4" else 180
+    t0 = time.perf_counter()
+    for name, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        cmd = ["timeout", "-s", "KILL", str(limit), rp, "--pmc", ctr, "--kernel-include-regex",
+               "k_sddmm", "--output-format", "csv", "-d", os.path.join(tmp, name), "-o", "run",
+               "--", sys.executable, os.path.join(ROOT, "tools", "prof_sddmm.py")] + wl
+        r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                           text=True)
+        if r.returncode != 0:
+            return None, {"status": f"rocprofv3 --pmc {ctr} failed (rc {r.returncode})",
+                          "stderr_tail": r.stderr[-300:]}
+    try:
+        out = subprocess.check_output([sys.executable, os.path.join(ROOT, "tools", "pmc_table.py"),
+                                       tmp], text=True)
+        full = json.loads(out)["full"]
+        fetch = 2.0 * full["FETCH_SIZE"] * 1024.0
+        write = full["WRITE_SIZE"] * 1024.0
+    except (subprocess.CalledProcessError, KeyError, ValueError) as e:
+        return None, {"status": f"PMC parse failed: {e}"}
+    shutil.rmtree(tmp, ignore_errors=True)
+    return round(fetch + write), {
+        "status": "measured in this run", "fetch_bytes": round(fetch), "write_bytes": round(write),
+        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
+                  "tools/prof_sddmm.py --iters 5, median over the fused launches; FETCH_SIZE "
+                  "KiB x 2 (gfx950) + WRITE_SIZE KiB",
+        "seconds": round(time.perf_counter() - t0, 1)}
+
+
 def main():
     args = parse()
-    import torch
-
     from bsmr import dist as D
 
     rank, world, local = D.env_rank_world()
+    # in-run PMC traffic (children, before this process touches the GPU; N=1 only)
+    args.pmc_result = pmc_traffic_inrun(args) if world == 1 else (None, None)
+    import torch
+
     if world > 1:
         # one rank per GPU; BSMR_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
         # multi-process path (ranks then share devices; their timings are not a measurement)
@@ -349,7 +406,13 @@ def main_single(args):
     value = flops_rank * world / (ms_per_step * 1e-3) / 1e9
     bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
     achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
-    traffic, traffic_src = traffic_for(args, K)
+    traffic, traffic_src = args.pmc_result
+    if traffic is None:  # a committed PMC summary measured on these kernel sources, if any
+        t2, src2 = traffic_for(args, K)
+        if t2 is not None:
+            traffic, traffic_src = t2, dict(src2, inrun=traffic_src)
+        elif traffic_src is not None and src2 is not None:
+            traffic_src = dict(traffic_src, committed=src2)
 
     kern, rby = kernel_name(st, st_after, K, dtype, args.layout)
     no_tiles = (kern.startswith("k_sddmm_rb") and
@@ -359,9 +422,9 @@ def main_single(args):
             "bytes_alg_per_launch": bytes_alg, "traffic_source": traffic_src}
     dtiles = st_after.get("dense_sampled_tiles", 0)
     if dtiles:  # sddmm.hip use_dense: whole 128 x 128 tiles on the matrix cores
-        ks = 2 if dtiles < 512 else 1  # sddmm_dense.hip launch_dense (BSMR_DENSE_KS unset)
-        kern = (f"k_sddmm_dense<{'f16' if dtype == 1 else 'bf16'},64,2,{ks}> (dense-sampled: "
-                f"{dtiles} non-empty 128 x 128 MFMA tiles, {4 * ks} waves per tile, K in 64-wide "
+        nw = 8 if dtiles < 512 else 4  # sddmm_dense.hip launch_dense (BSMR_DENSE_KS unset)
+        kern = (f"k_sddmm_dense<{'f16' if dtype == 1 else 'bf16'},64,2,{nw}> (dense-sampled: "
+                f"{dtiles} non-empty 128 x 128 MFMA tiles, {nw} waves per tile, K in 64-wide "
                 "LDS-DMA chunks, stored entries sampled from the fp32 tile)")
         flops_tiles = 2.0 * dtiles * 128 * 128 * K
         ach = flops_tiles / (ms_per_step * 1e-3) / 1e12
