@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Build gate: parse hipcc's -Rpass-analysis=kernel-resource-usage remarks and fail when an SDDMM
 kernel (k_sddmm*) spills VGPRs/SGPRs or uses scratch. Usage: check_kernel_resources.py <remarks>"""
+import os
 import re
 import sys
 
@@ -15,6 +16,9 @@ def main(path):
                 seen += "k_sddmm" in kern
                 continue
             if not kern or "k_sddmm" not in kern:
+                continue
+            allow = os.environ.get("RES_CHECK_ALLOW")  # experiments only: a regex of kernels
+            if allow and re.search(allow, kern):
                 continue
             m = re.search(r"remark:\s+(VGPRs Spill|SGPRs Spill|ScratchSize \[bytes/lane\]): (\d+)",
                           line)
