@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libbsmr_amd.so")
+# BSMR_LIB_PATH: another build of the same library (A/B timing of kernel variants only)
+LIB_PATH = os.environ.get("BSMR_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libbsmr_amd.so")
 
 F32, F16, BF16 = 0, 1, 2
 
