@@ -181,21 +181,22 @@ constexpr u32 CL_WAVES = 16;    // waves per tile workgroup
 constexpr u32 CL_SUB = 64;      // positions per evaluation sub-batch (4 per wave)
 constexpr u32 CL_WIN = 256;     // ready positions per window
 constexpr u32 CL_LDS_BUDGET = 148 * 1024;  // representatives (the control block follows)
-// evaluation codes (per position, per sub-batch): the tile cluster where the walk stopped
-constexpr u32 EV_REJECT = 0xFFu, EV_ACCEPT = 0x100u, EV_EXACT = 0x200u;
+// accept chains the leader resolves alone (re-evaluating one position at a time) before it
+// hands the rest of a sub-batch back to all waves
+constexpr u32 CL_LEADER_EVALS = 16;
 
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 // control block after the representatives
 struct ClusterCtl {
     u32 todo[CL_WIN];      // unassigned ready positions of the window
-    u32 res[CL_WIN];       // evaluation code per todo slot (current sub-batch)
+    u32 res[CL_WIN];       // verdict masks per todo slot (eval_row; current sub-batch)
     uint4 meta[CL_WIN];    // per todo slot: encoding offset, #blocks, SC, S1C of its row
     float inrf[CL_TMAX];   // 1 / nr per tile cluster (0 for an empty or zero-norm slot)
     float nr[CL_TMAX];     // sqrtf(SR)
     u32 SR[CL_TMAX];       // kept-block sum of squares of the representative (u32 wrap)
     u64 S1R[CL_TMAX];      // kept-block sum of the representative
-    u32 ntodo, t, nact, done, i;
+    u32 ntodo, t, nact, done, i, nact_eval;
     u64 nexact, ntotal;
 };
 
@@ -281,14 +282,15 @@ __device__ __forceinline__ double wave_sum8(const double (&v)[CL_TMAX]) {
     return s;
 }
 
-// one wave: walk tile clusters [cfrom, nact) for the row with metadata m (encoding offset,
-// #blocks, SC, S1C) and first encoding chunk pre (entries l + 64u, 0 past the row) with the
-// estimate; returns EV_ACCEPT | c, EV_EXACT | c (guard band: the exact emulation must decide c)
-// or EV_REJECT. Estimate: fp32 products and minima (relative error <= 2 ulp each), summed in
-// fp32 over 4 entries and in double beyond: < 5e-7 relative in total, far inside GUARD.
+// one wave: the verdicts of tile clusters [0, nact) on the row with metadata m (encoding offset,
+// #blocks, SC, S1C) and first encoding chunk pre (entries l + 64u, 0 past the row), from the
+// estimate: bit c of the low byte = accept, of the second byte = guard band (the exact emulation
+// must decide c); neither = reject. Estimate: fp32 products and minima (relative error <= 2 ulp
+// each), summed in fp32 over 4 entries and in double beyond: < 5e-7 relative in total, far
+// inside GUARD.
 template <u32 TS>
 __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl& C, uint4 m,
-                        const u32 (&pre)[4], u32 cfrom, u32 nact) {
+                        const u32 (&pre)[4], u32 nact) {
     const u32 l = lane_id();
     const u32 b0 = m.x, nb = m.y, scr = m.z, s1c = m.w;
     const float nc = sqrtf(static_cast<float>(scr));
@@ -349,28 +351,32 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
         }
         red = wave_sum8(mn);
     }
-    for (u32 c = cfrom; c < nact; ++c) {
+    u32 acc = 0, ex = 0;
+    for (u32 c = 0; c < nact; ++c) {
         const u32 SR = C.SR[c];
         if (SR == 0 && scr == 0) {
-            if (1.0f > a.alpha) return EV_ACCEPT | c;
+            if (1.0f > a.alpha) acc |= 1u << c;
             continue;
         }
         if (SR == 0 || scr == 0) {
-            if (0.0f > a.alpha) return EV_ACCEPT | c;
+            if (0.0f > a.alpha) acc |= 1u << c;
             continue;
         }
-        if (!est) return EV_EXACT | c;
+        if (!est) {
+            ex |= 1u << c;
+            continue;
+        }
         const double mnc = readlane_f64(red, 8 * c);
         const double mx = static_cast<double>(C.S1R[c]) / C.nr[c] + static_cast<double>(s1c) / nc - mnc;
         const double sim = mnc / mx;
         const double ad = static_cast<double>(a.alpha);
         if (fabs(sim - ad) > GUARD) {
-            if (sim > ad) return EV_ACCEPT | c;
-            continue;
+            if (sim > ad) acc |= 1u << c;
+        } else {
+            ex |= 1u << c;
         }
-        return EV_EXACT | c;
     }
-    return EV_REJECT;
+    return acc | (ex << 8);
 }
 
 __device__ __forceinline__ void load_chunk0(const ClusterArgs& a, uint4 m, u32 (&ent)[4]) {
@@ -606,54 +612,77 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                         m = C.meta[jn];
                         load_chunk0(a, m, pre);
                     }
-                    const u32 r = eval_row<TS>(a, reps, C, mc, cur, 0, nact);
+                    const u32 r = eval_row<TS>(a, reps, C, mc, cur, nact);
                     if (l == 0) C.res[j] = r;
                     j = jn;
                 }
             }
             __syncthreads();
             if (w == 0) {
-                u32 j = t;
+                // the sequential rule over the sub-batch. Verdicts of clusters whose
+                // representative changed since the evaluation (dirty: accepts, new clusters)
+                // are stale: a position whose walk reaches one is evaluated again by this wave
+                // (accept chains), up to CL_LEADER_EVALS times; after a new cluster, or past
+                // that budget, the rest goes back to all waves
+                u32 j = t, dirty = 0, budget = CL_LEADER_EVALS;
                 u64 nex = 0, ntot = 0;
                 while (j < tend) {
-                    // plain rejects of a full tile up to the first event, stored lane-parallel
-                    const u32 n = tend - j;
-                    const u32 r = l < n ? C.res[j + l] : EV_REJECT;
-                    const u64 ev = __ballot(l < n && (r != EV_REJECT || C.nact < T));
-                    const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : n;
-                    if (l < e) st_agent(&a.state[C.todo[j + l]], klast);
-                    ntot += static_cast<u64>(e) * C.nact;
-                    j += e;
-                    if (j >= tend) break;
-                    // the event: exact emulation where the estimate is in the guard band, then
-                    // an accept or a new cluster; the positions after it are evaluated again
+                    if (dirty == 0) {
+                        // plain rejects of a full tile up to the first other verdict, stored
+                        // lane-parallel
+                        const u32 n = tend - j;
+                        const u32 r = l < n ? C.res[j + l] : 0u;
+                        const u64 ev = __ballot(l < n && (r != 0u || C.nact < T));
+                        const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : n;
+                        if (l < e) st_agent(&a.state[C.todo[j + l]], klast);
+                        ntot += static_cast<u64>(e) * C.nact;
+                        j += e;
+                        if (j >= tend) break;
+                    }
                     const u32 p = C.todo[j];
                     const uint4 m = C.meta[j];
-                    u32 rr = C.res[j];
-                    while ((rr & EV_EXACT) != 0) {
-                        const u32 c = rr & 0xFFu;
-                        ++nex;
-                        if (exact(m, c)) {
-                            rr = EV_ACCEPT | c;
-                        } else if (c + 1 < C.nact) {
+                    u32 r = C.res[j];
+                    bool fresh = false;
+                    const u32 na = C.nact;
+                    u32 c = 0, take = ~0u, nex_p = 0;  // exact evaluations of this walk
+                    bool stop = false;  // the rest to all waves
+                    for (; c < na; ++c) {
+                        if (!fresh && (((dirty >> c) & 1u) || c >= nact)) {
+                            if (budget == 0) {
+                                stop = true;
+                                break;
+                            }
+                            --budget;
                             u32 pre[4];
                             load_chunk0(a, m, pre);
-                            rr = eval_row<TS>(a, reps, C, m, pre, c + 1, C.nact);
-                        } else {
-                            rr = EV_REJECT;
+                            r = eval_row<TS>(a, reps, C, m, pre, na);
+                            fresh = true;
+                        }
+                        if ((r >> c) & 1u) {
+                            take = c;
+                            break;
+                        }
+                        if ((r >> (8 + c)) & 1u) {
+                            ++nex_p;
+                            if (exact(m, c)) {
+                                take = c;
+                                break;
+                            }
                         }
                     }
+                    if (stop) break;  // this position is walked again by the next round
+                    nex += nex_p;
                     ++j;
-                    if (rr & EV_ACCEPT) {
-                        const u32 c = rr & 0xFFu;
-                        ntot += c + 1;
-                        accept(p, m, c);
-                        break;
+                    if (take != ~0u) {
+                        ntot += take + 1;
+                        accept(p, m, take);
+                        dirty |= 1u << take;
+                        continue;
                     }
-                    ntot += C.nact;
-                    if (C.nact < T) {
+                    ntot += na;
+                    if (na < T) {
                         new_cluster(p, m);
-                        break;
+                        break;  // a new cluster: the rest of the sub-batch to all waves
                     }
                     if (l == 0) st_agent(&a.state[p], klast);
                 }
