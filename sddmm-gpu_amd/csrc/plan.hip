@@ -1446,7 +1446,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             lo = hi;
             st0[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * k / NCR);
             st1[i] = t0 + static_cast<u32>(static_cast<u64>(nt) * (k + 1) / NCR);
-            cost[i] = (se1[i] - se0[i]) + spc[i] + 16.0 * (st1[i] - st0[i]);
+            cost[i] = (se1[i] - se0[i]) + piece_weight * spc[i] + 16.0 * (st1[i] - st0[i]);
         }
     }
     // chunks. A row block is split by the column ranges (its items then read B from their own

@@ -55,6 +55,11 @@ struct Plan {
     bool l2_range_user = false;  // BSMR_L2_RANGE_KB given: then also for staged layouts
     // entries per column-run piece of the row-block layout (<= RB_PIECE_MAX; BSMR_PIECE_MAX)
     u32 piece_max = RB_PIECE_MAX;
+    // a column-run piece's weight in the item cost model, in entries (BSMR_PIECE_WEIGHT): each
+    // piece gathers a whole B row. Measured (profiles/r02c/piece_weight.txt): C2 11.60 us at 1,
+    // 11.05 at 4, 11.15 at 8 (items of the short last row block, all short pieces, were the
+    // launch's tail); C4 x0.5 -0.8 %; C3 unchanged
+    double piece_weight = 4.0;
     // row-block results staged in LDS and written in CSR order per item, for P larger than
     // out_staged_min bytes (BSMR_OUT_STAGED: 0 never, 1 always, else auto). Measured
     // (profiles/r02ab1): C3 cop20k-like (P 10 MB) 77.0 -> 72.0 us, C4 reddit-like x0.5 (232 MB)
