@@ -243,27 +243,44 @@ def kernel_name(st, st_after, K, dtype, layout):
 
 
 def traffic_for(args, K):
-    """roofline.traffic: HBM bytes per launch from the committed PMC summary of this config
-    (tools/pmc_traffic.py), only if it was measured on the kernel sources of this tree (their
-    sha256 is recorded in the file); None otherwise."""
-    tj = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{args.config}_K{K}.json")
-    if not os.path.exists(tj):
-        return None, None
-    with open(tj) as f:
-        t = json.load(f)
+    """roofline.traffic fallback: HBM bytes per launch from a committed PMC summary of this config
+    (tools/pmc_traffic.py), used only if it was measured on the kernel sources of this tree (their
+    sha256 is recorded in the file); None otherwise. Candidates: --traffic-json, else
+    profiles/traffic_<config>_K<K>.json and profiles/*/<label>/traffic.json (label C2, C3, C4,
+    C5u, C5b), newest round first."""
+    import glob
     import hashlib
 
-    srcs = t.get("kernel_sources_sha256")
-    if not srcs:
-        return None, {"file": os.path.relpath(tj, ROOT), "status": "no source hash: not used"}
-    for rel, h in srcs.items():
-        with open(os.path.join(ROOT, rel), "rb") as f:
-            if hashlib.sha256(f.read()).hexdigest() != h:
-                return None, {"file": os.path.relpath(tj, ROOT),
-                              "status": f"stale: {rel} changed since the PMC run"}
-    return t.get("hbm_bytes_per_launch"), {"file": os.path.relpath(tj, ROOT),
-                                           "measured_on": t.get("measured_on"),
-                                           "status": "kernel sources match"}
+    label = args.config + ({"uniform": "u", "block": "b"}[args.mask] if args.config == "C5" else "")
+    if args.traffic_json:
+        cands = [args.traffic_json]
+    else:
+        cands = [os.path.join(ROOT, "profiles", f"traffic_{args.config}_K{K}.json")]
+        cands += sorted(glob.glob(os.path.join(ROOT, "profiles", "*", label, "traffic.json")),
+                        reverse=True)
+    last = None
+    for tj in cands:
+        if not os.path.exists(tj):
+            continue
+        with open(tj) as f:
+            t = json.load(f)
+        srcs = t.get("kernel_sources_sha256")
+        if not srcs:
+            last = {"file": os.path.relpath(tj, ROOT), "status": "no source hash: not used"}
+            continue
+        stale = None
+        for rel, h in srcs.items():
+            with open(os.path.join(ROOT, rel), "rb") as f:
+                if hashlib.sha256(f.read()).hexdigest() != h:
+                    stale = rel
+                    break
+        if stale:
+            last = {"file": os.path.relpath(tj, ROOT), "status": f"stale: {stale} changed since the PMC run"}
+            continue
+        return t.get("hbm_bytes_per_launch"), {"file": os.path.relpath(tj, ROOT),
+                                               "measured_on": t.get("measured_on"),
+                                               "status": "kernel sources match"}
+    return None, last
 
 
 def pmc_traffic_inrun(args):
