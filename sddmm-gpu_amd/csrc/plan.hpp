@@ -203,8 +203,10 @@ struct Plan {
         DevBuf<u32> off, loc, out;  // loc = local row << 7 | local column; out = CSR position
     };
     mutable DenseLayout dense;
-    int dense_ks = 0;  // BSMR_DENSE_KS: 1 / 2 wave sets per tile, else by tile count
-    int dense_ns = 2;  // BSMR_DENSE_NS: LDS stages of the split-k dense launch (2..5)
+    // BSMR_DENSE_KS: dense-sampled workgroups of 1 = four waves (64 x 64 quadrants), 2 = eight
+    // waves (64 x 32 blocks), else eight below 512 non-empty tiles
+    int dense_ks = 0;
+    int dense_ns = 2;  // BSMR_DENSE_NS: LDS stages of the eight-wave dense launch (2..5)
     int build_dense_layout() const;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);

@@ -310,7 +310,8 @@ int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     // (KC, NS) = (64, 2): two workgroups per CU. Measured (tools/gpu_dense_stages.sh history,
     // r01q): 4 stages at one workgroup per CU and KC = 32 at 2-4 stages / 2-4 workgroups were
     // all slower (C5 uniform 10.6-12.1 us vs 8.8-9.8)
-    // split-k wave sets when the tiles fill at most one workgroup per CU (C5: 256 tiles)
+    // eight waves (64 x 32 blocks, two per SIMD) when the tiles fill at most one workgroup per CU
+    // (C5: 256 tiles)
     const bool ks2 = p.dense_ks == 2 || (p.dense_ks != 1 && D.nonempty < 512);
     if (ks2) {
         const bool f16 = dtype == BSMR_F16;

@@ -96,6 +96,30 @@ def test_dense_sampled_half(monkeypatch, case, K, dtype, force):
     assert O.check_data(ref, P) == 0
 
 
+@pytest.mark.parametrize("env,K,dtype", [
+    ({"BSMR_DENSE_KS": "1"}, 256, F16),    # four waves, 64 x 64 quadrants (>= 512 tiles by default)
+    ({"BSMR_DENSE_KS": "1"}, 320, BF16),
+    ({"BSMR_DENSE_NS": "3"}, 320, BF16),   # eight waves, 3-5 LDS stages (BSMR_DENSE_NS)
+    ({"BSMR_DENSE_NS": "4"}, 256, F16),
+    ({"BSMR_DENSE_NS": "5"}, 128, BF16),   # fewer chunks than stages
+    ({"BSMR_DENSE_NS": "5"}, 512, F16),
+])
+def test_dense_sampled_variants(monkeypatch, env, K, dtype):
+    """Every wave/stage form of the dense-sampled launch (sddmm_dense.hip launch_dense) gives the
+    oracle's values on a ragged 300 x 300 pattern (edge tiles read clamped rows)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    M, N, rp, ci = synth.uniform_mask(300, 0.2, seed=11)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    conv = to_bf16_bits if dtype == BF16 else to_f16_bits
+    Ab, Ar = conv(make_data(M * K))
+    Bb, Br = conv(make_data(N * K)[::-1].copy())
+    P = run_half(plan, Ab, Bb, K, len(ci), dtype)
+    assert np.isfinite(P).all()
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, Ar, Br)
+    assert O.check_data(ref, P) == 0
+
+
 def test_dlmc_like_bf16_k512():
     M, N, rp, ci = synth.uniform_mask(2048, 0.1, seed=7)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
