@@ -933,8 +933,11 @@ int rb_slot(const Plan& p, u32 K, int dtype) {
 // fp16/bf16 patterns dense enough for whole MFMA tiles (sddmm_dense.hip)
 bool use_dense(const Plan& p, u32 K, int dtype) {
     // layout auto only (BSMR_LAYOUT_ROWBLOCK / _COLMAJOR force those launches)
-    // not for tile-dominated plans (16 x 16 block masks: the column-major tile launch)
-    if (static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16) return false;
+    // tile-dominated plans (16 x 16 block masks) keep the column-major tile launch below K = 512:
+    // a 128 x 128 tile's fixed prologue and epilogue only pay off over long K (C5 block mask,
+    // bf16: dense 8.2 vs 8.9 us at K = 512, 5.95 vs 5.35 at 256, 4.7 vs 3.8 at 128;
+    // profiles/r02c/dense_blockmask_ab.txt)
+    if (K < 512 && static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16) return false;
     return p.use_rowblock && !p.force_rowblock && dtype != BSMR_F32 && K % 64 == 0 &&
            static_cast<double>(p.nnz) >= static_cast<double>(p.dense_min) * p.M * static_cast<double>(p.N);
 }
