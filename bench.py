@@ -7,16 +7,20 @@ the plan of the C2 workload of BASELINE.json: nips-like 1,500 x 12,419 pattern w
 Reordering runs once before timing and is reported separately (the reference's GFLOP/s excludes it
 too, Logger.hpp:178-180). Inputs are resident in HBM when the timed region starts.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): row-panel
-shards of ONE global BSMR plan (bsmr/dist.py). Rank 0 builds the plan and
-broadcasts its row stage (the clustering result) over RCCL; every rank rebuilds the column stage
-from it, cuts the same contiguous panel ranges, uploads only its panels' A rows and runs
-bsmr_sddmm_panels_local; B is broadcast once from rank 0 over RCCL (xGMI); after timing P is
-sum-reduced to rank 0 and checked against the product's host SDDMM (checkData rule).
-  * C2 (default): weak scaling. The global pattern is N copies of the nips-like pattern stacked
-    vertically, copy b with its columns relabelled by a random permutation (synth.stack_copies),
-    so per-GPU work stays one C2 while the plan, the cut and the split are real.
-  * C3/C4/C5: strong scaling of the one matrix (C4: the north_star reddit split).
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): S sharded by
+row panels (bsmr/dist.py); B is broadcast once from rank 0 over RCCL (xGMI), each
+rank holds only its rows of A, and after timing P is sum-reduced to rank 0 and checked against the
+product's host SDDMM (checkData rule). Two splits (--shard):
+  * global (C3/C4/C5 default: strong scaling of the one matrix, C4 = the north_star reddit split):
+    row-panel shards of ONE global BSMR plan. Rank 0 builds the plan and broadcasts its row stage
+    (the clustering result) over RCCL; every rank rebuilds the column stage from it, cuts the same
+    contiguous panel ranges, uploads its panels' A rows and runs bsmr_sddmm_panels_local.
+  * local (C2 default: weak scaling): the global pattern is N copies of the nips-like pattern
+    stacked vertically, copy b with its columns relabelled by a random permutation
+    (synth.stack_copies), cut into N contiguous original row panels of equal stored entries (=
+    the copies); each rank builds the BSMR plan of its own panel and runs bsmr_sddmm on it, so
+    per-GPU work stays one C2. (A shard of one global plan mixes the copies' clusters: slower,
+    see main_sharded_local.)
 No collective in the timed loop; value = all ranks' flops / the slowest rank's time.
 
 Other BASELINE.json configs (extra measurements, not the driver's line): --config C3 (cop20k-like,
@@ -65,6 +69,11 @@ def parse():
                          "(FETCH_SIZE, WRITE_SIZE) over tools/prof_sddmm.py on the same workload, "
                          "run as child processes before this process touches the GPU (auto: at "
                          "N=1 when rocprofv3 is on PATH)")
+    ap.add_argument("--shard", default="auto", choices=["auto", "global", "local"],
+                    help="multi-GPU split: global = row-panel shards of one global BSMR plan "
+                         "(rank 0 clusters, row stage broadcast); local = contiguous original row "
+                         "panels of S balanced by stored entries, each rank clustering its own "
+                         "panel; auto = local for the C2 weak-scaling copies, global otherwise")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -514,7 +523,11 @@ def sharded_workload(args, world):
 
 
 def main_sharded(args, rank, world):
-    """Row-panel shards of one global plan over `world` ranks (bsmr/dist.py)."""
+    """Row-panel shards over `world` ranks (bsmr/dist.py): of one global plan (--shard global),
+    or contiguous original row panels each planned on its own rank (--shard local)."""
+    mode = args.shard if args.shard != "auto" else ("local" if args.config == "C2" else "global")
+    if mode == "local":
+        return main_sharded_local(args, rank, world)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -646,6 +659,153 @@ def main_sharded(args, rank, world):
             "ms_per_step": [round(x, 5) for x in ms_all],
             "imbalance_max_over_mean": round(ms_per_step / mean_ms, 3),
             "kernel": "bsmr_sddmm_panels_local -> " + kern,
+        },
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                     "frac": round(achieved / (HBM_PEAK_GBS * world), 4), "traffic": None,
+                     "kernel": kern, "bytes_alg_per_launch": bytes_alg,
+                     "note": "whole-job algorithmic bytes per step over the slowest rank's time, "
+                             "against world x 8 TB/s"},
+        "checkData_errors_gathered_P": nerr,
+    }
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+
+
+def main_sharded_local(args, rank, world):
+    """S cut into `world` contiguous original row panels of equal stored entries; rank r clusters
+    and lays out its own panel (a local BSMR plan over rows [r0, r1)), stages only those A rows,
+    receives B once over RCCL and writes P[rowptr[r0]:rowptr[r1]] (contiguous CSR positions), so P
+    assembles by a sum-reduce. For the C2 weak-scaling copies the panels are exactly the copies:
+    a shard of one global plan instead interleaves the copies' clusters (the BSMR cluster order
+    follows dispersion, which the copies share), so its row blocks mix unrelated column sets
+    (tools/shard_sim.py --copies N --local, each shard timed alone on one GPU: slowest shard at
+    N = 2 / 4 / 8 local 11.5 / 11.4 / 11.8 us, global 11.7 / 13.4 / 13.5 us; one C2 11.2 us;
+    profiles/r02c/weak_scaling/)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from bsmr import F32, Plan, check_data, make_data, sddmm_cpu
+    from bsmr import dist as D
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    (M, N, rp, ci), K, dtype, desc, scaling = sharded_workload(args, world)
+    nnz = len(ci)
+    rp64 = np.asarray(rp, dtype=np.int64)
+    r0, r1 = D.row_range_cut(rp64, rank, world)
+    e0, e1 = int(rp64[r0]), int(rp64[r1])
+    rp_loc = (rp64[r0:r1 + 1] - e0).astype(np.uint32)
+    ci_loc = np.ascontiguousarray(np.asarray(ci)[e0:e1], dtype=np.uint32)
+    t0 = time.perf_counter()
+    plan = Plan(max(r1 - r0, 1), N, rp_loc if r1 > r0 else np.zeros(2, np.uint32), ci_loc,
+                alpha=args.alpha, delta=args.delta, layout=args.layout)
+    plan_s = time.perf_counter() - t0
+    st = plan.stats()
+
+    tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
+    # A partitioned: the makeData stream is a function of the row, so every rank derives its own
+    # rows locally (nothing of A is sent)
+    A = make_data(M * K)
+    dA = torch.from_numpy(np.ascontiguousarray(A[r0 * K:max(r1, r0 + 1) * K])).to(dev).to(tdt)
+    if rank == 0:
+        B = make_data(N * K)
+        dB = torch.from_numpy(B).to(dev).to(tdt)
+    else:
+        B = None
+        dB = torch.empty(N * K, dtype=tdt, device=dev)
+    dist.barrier()
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
+    D.broadcast_(dB, 0)
+    torch.cuda.synchronize()
+    bcast_ms = (time.perf_counter() - tb) * 1e3
+    dP_loc = torch.zeros(max(e1 - e0, 1), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        if e1 > e0:
+            plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP_loc.data_ptr(), stream=sp, dtype=dtype)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    e_0 = torch.cuda.Event(enable_timing=True)
+    e_1 = torch.cuda.Event(enable_timing=True)
+    e_0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e_1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    ms_mine = e_0.elapsed_time(e_1) / args.steps
+    ms_all = D.all_values(ms_mine, dev)
+    ms_per_step = max(ms_all)  # whole-job time = slowest rank
+    entries_all = D.all_values(e1 - e0, dev)
+    rows_all = D.all_values(r1 - r0, dev)
+    plan_all = D.all_values(plan_s, dev)
+    dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
+    if e1 > e0:
+        dP[e0:e1] = dP_loc[:e1 - e0]
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    P = D.gather_p(dP, 0)  # sum-reduce: each output written by exactly one rank
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    st_after = plan.stats()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    if dtype == F32:
+        Ar, Br = A, B
+    else:
+        Ar = torch.from_numpy(A).to(tdt).float().numpy()
+        Br = dB.float().cpu().numpy()
+    ref = sddmm_cpu(M, N, rp, ci, K, Ar, Br,
+                    threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    nerr = check_data(ref, P)
+
+    flops = 2.0 * nnz * K
+    value = flops / (ms_per_step * 1e-3) / 1e9
+    s = 4 if dtype == F32 else 2
+    bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
+    achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
+    kern, _ = kernel_name(st, st_after, K, dtype, args.layout)
+    mean_ms = sum(ms_all) / world
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": {0: "f32", 1: "f16", 2: "bf16"}[dtype],
+        "data": "synthetic",
+        "config": {
+            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}",
+            "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
+            "parallelism": (f"row-panel shards x{world} of S in original row order (contiguous "
+                            "panels of equal stored entries), each rank's BSMR plan built on its "
+                            "own panel, A rows local, B broadcast once (RCCL), P sum-reduced to "
+                            "rank 0"),
+            "shard_mode": "local",
+            "backend": dist.get_backend(),
+            "plan_build_s_max": round(max(plan_all), 3),
+            "b_broadcast_ms": round(bcast_ms, 3),
+            "p_gather_ms": round(gather_ms, 3),
+        },
+        "shards": {
+            "rows": [int(x) for x in rows_all],
+            "entries": [int(x) for x in entries_all],
+            "ms_per_step": [round(x, 5) for x in ms_all],
+            "imbalance_max_over_mean": round(ms_per_step / mean_ms, 3),
+            "kernel": "bsmr_sddmm (rank-local plan) -> " + kern,
         },
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS * world, "unit": "GB/s",

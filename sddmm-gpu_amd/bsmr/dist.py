@@ -170,6 +170,19 @@ def distribute_plan(M, N, rowptr, colidx, device, alpha=0.3, delta=0.3, layout="
     return plan, info
 
 
+def row_range_cut(rowptr, rank, world):
+    """Original rows [r0, r1) of `rank` when S is cut into `world` contiguous row panels of
+    (nearly) equal stored entries (the cut is the first row whose CSR offset reaches each
+    target, so equal blocks such as stacked copies split exactly at their boundaries)."""
+    rp = np.asarray(rowptr, dtype=np.int64)
+    M, nnz = len(rp) - 1, int(rp[-1])
+    cuts = [0] + [min(M, int(np.searchsorted(rp, nnz * r // world, side="left")))
+                  for r in range(1, world)] + [M]
+    for r in range(1, world + 1):
+        cuts[r] = max(cuts[r], cuts[r - 1])
+    return cuts[rank], cuts[rank + 1]
+
+
 def shard_a_rows(A, K, reordered_rows, p0, p1):
     """The A rows of reordered positions [16 p0, min(16 p1, R)) in that order (host, row-major):
     the dA_local of bsmr_sddmm_panels_local."""

@@ -194,8 +194,11 @@ def reddit_like(scale=1.0, seed=20250803):
 def stack_copies(M, N, rowptr, colidx, copies, seed=20251016):
     """Weak-scaling workload: `copies` row blocks, block b = the pattern with its columns relabelled
     by a random permutation of [0, N) (block 0 unchanged), so the blocks' rows are as unlike each
-    other as the pattern's own rows and each block carries the pattern's work. copies = 1 returns
-    the pattern itself."""
+    other as the pattern's own rows and each block carries the pattern's work. Every row's columns
+    are re-sorted after the relabelling, as in a .mtx file loaded by the reference (ascending within
+    a row): unsorted rows interleave the XCD column ranges inside each row's CSR segment, so every
+    128-byte line of P would be written by several L2s (one copy: 14.9 vs 11.2 us,
+    tools/copy_order_check.py). copies = 1 returns the pattern itself."""
     rowptr = np.asarray(rowptr, dtype=np.uint32)
     colidx = np.asarray(colidx, dtype=np.uint32)
     if copies == 1:
@@ -208,7 +211,10 @@ def stack_copies(M, N, rowptr, colidx, copies, seed=20251016):
     for b in range(copies):
         perm = np.arange(N, dtype=np.uint32) if b == 0 else rng.permutation(N).astype(np.uint32)
         rp[1 + b * M: 1 + (b + 1) * M] = rowptr[1:].astype(np.uint64) + b * nnz
-        ci[b * nnz:(b + 1) * nnz] = perm[colidx]
+        cb = perm[colidx]
+        for r in range(M):  # ascending columns within each row
+            cb[rowptr[r]:rowptr[r + 1]].sort()
+        ci[b * nnz:(b + 1) * nnz] = cb
     if rp[-1] >= 2 ** 32:
         raise ValueError("stack_copies: more than 2^32 stored entries")
     return copies * M, N, rp.astype(np.uint32), ci

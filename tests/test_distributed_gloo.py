@@ -79,6 +79,20 @@ def _worker(rank, world, port, q):
         res["p_errors"] = O.check_data(ref, Pg)
         res["p_written"] = int(np.count_nonzero(Pg))
         res["nnz"] = len(ci)
+    # the local split (bench.py --shard local, the C2 weak-scaling default): contiguous original
+    # row panels of equal stored entries (= the stacked copies), each rank's outputs written at
+    # their contiguous CSR positions, assembled by the same sum-reduce
+    q0, q1 = D.row_range_cut(rp, rank, world)
+    res["local_cut"] = (q0, q1)
+    P2 = np.zeros(len(ci), np.float32)
+    A_rows = np.asarray(A).reshape(-1, K)[q0:q1]  # only this rank's rows of A
+    for j, row in enumerate(range(q0, q1)):
+        for e in range(rp[row], rp[row + 1]):
+            P2[e] = np.dot(A_rows[j].astype(np.float64), Bf[ci[e] * K:(ci[e] + 1) * K])
+    Pg2 = D.gather_p(torch.from_numpy(P2), 0)
+    if rank == 0:
+        res["p2_errors"] = O.check_data(ref, Pg2)
+        res["p2_written"] = int(np.count_nonzero(Pg2))
     import torch.distributed as dist
     dist.destroy_process_group()
     q.put(res)
@@ -104,3 +118,23 @@ def test_gloo_world2_row_stage_shards_and_p_gather():
     (a0, a1), (b0, b1) = r0["cut"], r1["cut"]
     assert a0 == 0 and a1 == b0 and a0 < a1 < b1
     assert r0["p_errors"] == 0 and r0["p_written"] == r0["nnz"]
+    assert r0["local_cut"] == (0, 300) and r1["local_cut"] == (300, 600)  # the two copies
+    assert r0["p2_errors"] == 0 and r0["p2_written"] == r0["nnz"]
+
+
+def test_row_range_cut():
+    """Contiguous row panels of (nearly) equal stored entries, exact at equal-block boundaries,
+    covering every row once, including empty rows and more ranks than non-empty rows."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "sddmm-gpu_amd"))
+    from bsmr import dist as D
+    rp = np.array([0, 5, 10, 15, 20], dtype=np.uint32)  # 4 rows of 5
+    assert [D.row_range_cut(rp, r, 2) for r in range(2)] == [(0, 2), (2, 4)]
+    assert [D.row_range_cut(rp, r, 4) for r in range(4)] == [(0, 1), (1, 2), (2, 3), (3, 4)]
+    rp = np.array([0, 0, 12, 12, 13, 20, 20], dtype=np.uint32)  # empty and uneven rows
+    for world in (1, 2, 3, 5, 8):
+        cuts = [D.row_range_cut(rp, r, world) for r in range(world)]
+        assert cuts[0][0] == 0 and cuts[-1][1] == 6
+        assert all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
+        assert all(a <= b for a, b in cuts)

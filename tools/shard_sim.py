@@ -8,6 +8,7 @@ the unsharded launch (checkData rule). B broadcast time is not included (bench.p
 measures it over RCCL).
 
     python3 tools/shard_sim.py --workload reddit_like --scale 0.5 --K 128
+    python3 tools/shard_sim.py --workload nips_like --copies 8   # bench --gpus 8 (C2 weak) rank by rank
 """
 import argparse
 import json
@@ -28,6 +29,12 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--copies", type=int, default=1,
+                    help="stack this many column-relabelled copies (bench.py's C2 weak scaling at "
+                         "--gpus copies; synth.stack_copies) and shard over world = copies only")
+    ap.add_argument("--local", action="store_true",
+                    help="also time bench.py --shard local: contiguous original row panels of equal "
+                         "stored entries, each on its own BSMR plan")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -38,6 +45,9 @@ def main():
 
     gen = getattr(synth, args.workload)
     M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
+    if args.copies > 1:
+        M, N, rp, ci = synth.stack_copies(M, N, rp, ci, args.copies)
+        args.worlds = str(args.copies)
     K = args.K
     code = {"f32": bsmr.F32, "f16": bsmr.F16, "bf16": bsmr.BF16}[args.dtype]
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
@@ -98,6 +108,31 @@ def main():
             "unwritten": int(np.isnan(P).sum()),
             "checkData_errors_vs_unsharded": O.check_data(P_full, P)}
         print(json.dumps({world: out["worlds"][world]}), file=sys.stderr, flush=True)
+    if args.local:
+        from bsmr import dist as D
+        rp64 = np.asarray(rp, dtype=np.int64)
+        for world in [int(w) for w in args.worlds.split(",")]:
+            ms, cl = [], []
+            for r in range(world):
+                r0, r1 = D.row_range_cut(rp64, r, world)
+                e0, e1 = int(rp64[r0]), int(rp64[r1])
+                lp = Plan(r1 - r0, N, (rp64[r0:r1 + 1] - e0).astype(np.uint32),
+                          np.ascontiguousarray(np.asarray(ci)[e0:e1], dtype=np.uint32),
+                          alpha=0.3, delta=0.3)
+                a_loc = dA[r0 * K:r1 * K].contiguous()
+                p_loc = torch.zeros(e1 - e0, dtype=torch.float32, device="cuda")
+                ms.append(timed(lambda: lp.sddmm(a_loc.data_ptr(), dB.data_ptr(), K,
+                                                 p_loc.data_ptr(), stream=s, dtype=code)))
+                cl.append(O.check_data(P_full[e0:e1], p_loc.cpu().numpy()))
+                del lp
+            slow = max(ms)
+            out["worlds"][f"local{world}"] = {
+                "shard_ms": [round(x, 5) for x in ms], "step_ms": round(slow, 5),
+                "imbalance": round(slow / (sum(ms) / len(ms)), 3),
+                "aggregate_GFLOP/s": round(flops / slow / 1e6, 1),
+                "checkData_errors_vs_unsharded": int(sum(cl))}
+            print(json.dumps({f"local{world}": out["worlds"][f"local{world}"]}), file=sys.stderr,
+                  flush=True)
     print(json.dumps(out))
 
 
