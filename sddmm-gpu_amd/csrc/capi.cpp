@@ -58,6 +58,8 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
     if (const char* pm = std::getenv("BSMR_PIECE_MAX"))
         p.piece_max = std::min<u32>(RB_PIECE_MAX, std::max(1, std::atoi(pm)));
     if (const char* pw = std::getenv("BSMR_PIECE_WEIGHT")) p.piece_weight = std::max(0.0, std::atof(pw));
+    if (const char* sw = std::getenv("BSMR_SHARD_PIECE_WEIGHT"))
+        p.shard_piece_weight = std::max(0.0, std::atof(sw));
     if (const char* dm = std::getenv("BSMR_DENSE_MIN")) p.dense_min = static_cast<float>(std::atof(dm));
     if (const char* orr = std::getenv("BSMR_ORIG_ROWS"))  // "0" never, "1" always, else auto
         p.orig_rows = orr[0] == '0' ? 0 : orr[0] == '1' ? 1 : -1;

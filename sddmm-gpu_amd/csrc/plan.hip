@@ -1594,7 +1594,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         ++L.nWorkItems;
         u64 ent = 0;
         for (u32 k = it.w; k < ends[i]; ++k) ent += (pieces[k].y >> 22) + 1;
-        L.rbCost[it.x] += static_cast<double>(ent) + (ends[i] - it.w) + 16.0 * (it.z - it.y) + RBr;
+        L.rbCost[it.x] += static_cast<double>(ent) + shard_piece_weight * (ends[i] - it.w) +
+                          16.0 * (it.z - it.y) + RBr;
     }
     L.nItems = static_cast<u32>(items.size());
     L.nPieces = static_cast<u32>(pieces.size());

@@ -60,6 +60,9 @@ struct Plan {
     // 11.05 at 4, 11.15 at 8 (items of the short last row block, all short pieces, were the
     // launch's tail); C4 x0.5 -0.8 %; C3 unchanged
     double piece_weight = 4.0;
+    // the same weight in the row-panel shard cost (RowBlockLayout::rbCost, bsmr_plan_shard):
+    // BSMR_SHARD_PIECE_WEIGHT
+    double shard_piece_weight = 4.0;
     // row-block results staged in LDS and written in CSR order per item, for P larger than
     // out_staged_min bytes (BSMR_OUT_STAGED: 0 never, 1 always, else auto). Measured
     // (profiles/r02ab1): C3 cop20k-like (P 10 MB) 77.0 -> 72.0 us, C4 reddit-like x0.5 (232 MB)
