@@ -225,6 +225,8 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     ({"BSMR_PIECE_ORDER": "1"}, 128, 0),
     ({"BSMR_PIECE_WEIGHT": "0"}, 128, 0),     # item cut by entries + tiles only
     ({"BSMR_PIECE_WEIGHT": "16"}, 256, 1),    # pieces dominate the item cost
+    ({"BSMR_SHARD_PIECE_WEIGHT": "1"}, 128, 0),   # shard cuts (checked below) by entries mostly
+    ({"BSMR_SHARD_PIECE_WEIGHT": "16"}, 64, 2),
     ({"BSMR_TILE_MIN_F32": "0"}, 32, 0),       # 128-byte rows, fp32 tiles on MFMA
     ({}, 32, 0),                               # 128-byte rows (8 rows per staged KiB)
     ({"BSMR_TILE_MIN_HALF": "0"}, 64, 1),      # 128-byte rows, half tiles on MFMA
