@@ -10,17 +10,17 @@ too, Logger.hpp:178-180). Inputs are resident in HBM when the timed region start
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): S sharded by
 row panels (bsmr/dist.py); B is broadcast once from rank 0 over RCCL (xGMI), each
 rank holds only its rows of A, and after timing P is sum-reduced to rank 0 and checked against the
-product's host SDDMM (checkData rule). Two splits (--shard):
-  * global (C3/C4/C5 default: strong scaling of the one matrix, C4 = the north_star reddit split):
-    row-panel shards of ONE global BSMR plan. Rank 0 builds the plan and broadcasts its row stage
-    (the clustering result) over RCCL; every rank rebuilds the column stage from it, cuts the same
-    contiguous panel ranges, uploads its panels' A rows and runs bsmr_sddmm_panels_local.
-  * local (C2 default: weak scaling): the global pattern is N copies of the nips-like pattern
-    stacked vertically, copy b with its columns relabelled by a random permutation
-    (synth.stack_copies), cut into N contiguous original row panels of equal stored entries (=
-    the copies); each rank builds the BSMR plan of its own panel and runs bsmr_sddmm on it, so
-    per-GPU work stays one C2. (A shard of one global plan mixes the copies' clusters: slower,
-    see main_sharded_local.)
+product's host SDDMM (checkData rule). C2 (default) is weak scaling: the global pattern is N
+copies of the nips-like pattern stacked vertically, copy b with its columns relabelled by a random
+permutation (synth.stack_copies), so per-GPU work stays one C2; C3/C4/C5 are strong scaling of the
+one matrix (C4 = the north_star reddit split). Two splits (--shard):
+  * local (default): N contiguous original row panels of equal stored entries (for C2 exactly the
+    copies); each rank builds the BSMR plan of its own panel and runs bsmr_sddmm on it.
+  * global: row-panel shards of ONE global BSMR plan. Rank 0 builds the plan and broadcasts its row
+    stage (the clustering result) over RCCL; every rank rebuilds the column stage from it, cuts the
+    same contiguous panel ranges, uploads its panels' A rows and runs bsmr_sddmm_panels_local.
+  Local is faster for both scalings (one-GPU rehearsal, tools/shard_sim.py, slowest of 8 shards:
+  C2 copies 11.8 vs 13.5 us, reddit-like x1 0.600 vs 0.726 ms; see main_sharded_local).
 No collective in the timed loop; value = all ranks' flops / the slowest rank's time.
 
 Other BASELINE.json configs (extra measurements, not the driver's line): --config C3 (cop20k-like,
@@ -73,7 +73,7 @@ def parse():
                     help="multi-GPU split: global = row-panel shards of one global BSMR plan "
                          "(rank 0 clusters, row stage broadcast); local = contiguous original row "
                          "panels of S balanced by stored entries, each rank clustering its own "
-                         "panel; auto = local for the C2 weak-scaling copies, global otherwise")
+                         "panel; auto = local (measured faster for C2 and C4: DESIGN.md section 7)")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -525,7 +525,7 @@ def sharded_workload(args, world):
 def main_sharded(args, rank, world):
     """Row-panel shards over `world` ranks (bsmr/dist.py): of one global plan (--shard global),
     or contiguous original row panels each planned on its own rank (--shard local)."""
-    mode = args.shard if args.shard != "auto" else ("local" if args.config == "C2" else "global")
+    mode = "global" if args.shard == "global" else "local"
     if mode == "local":
         return main_sharded_local(args, rank, world)
     import numpy as np
@@ -642,6 +642,7 @@ def main_sharded(args, rank, world):
                             "row stage broadcast over RCCL, column stage rebuilt per rank), A "
                             "rows local to their shard, B broadcast once (RCCL), P sum-reduced "
                             "to rank 0"),
+            "shard_mode": "global",
             "backend": dist.get_backend(),
             "num_clusters": st["num_clusters"], "num_row_panels": st["num_row_panels"],
             "plan_build_s": round(pinfo["plan_build_s"], 3),
@@ -676,9 +677,13 @@ def main_sharded_local(args, rank, world):
     """S cut into `world` contiguous original row panels of equal stored entries; rank r clusters
     and lays out its own panel (a local BSMR plan over rows [r0, r1)), stages only those A rows,
     receives B once over RCCL and writes P[rowptr[r0]:rowptr[r1]] (contiguous CSR positions), so P
-    assembles by a sum-reduce. For the C2 weak-scaling copies the panels are exactly the copies:
-    a shard of one global plan instead interleaves the copies' clusters (the BSMR cluster order
-    follows dispersion, which the copies share), so its row blocks mix unrelated column sets
+    assembles by a sum-reduce. No plan crosses ranks, and every rank clusters only its own rows.
+    C4 (reddit-like x1, 8 shards timed alone on one GPU): slowest shard 0.600 ms, imbalance 1.02,
+    against 0.726 ms / 1.19 for shards of the global plan, whose leading panels hold the sparse
+    low-dispersion rows (profiles/r02c/c4_shards/). For the C2 weak-scaling copies the panels are
+    exactly the copies: a shard of one global plan instead interleaves the copies' clusters (the
+    BSMR cluster order follows dispersion, which the copies share), so its row blocks mix unrelated
+    column sets
     (tools/shard_sim.py --copies N --local, each shard timed alone on one GPU: slowest shard at
     N = 2 / 4 / 8 local 11.5 / 11.4 / 11.8 us, global 11.7 / 13.4 / 13.5 us; one C2 11.2 us;
     profiles/r02c/weak_scaling/)."""

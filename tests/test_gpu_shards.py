@@ -141,7 +141,8 @@ def _free_port():
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("extra", [["--config", "C2"], ["--config", "C2", "--shard", "global"],
-                                   ["--config", "C4", "--scale", "0.05"]])
+                                   ["--config", "C4", "--scale", "0.05"],
+                                   ["--config", "C4", "--scale", "0.05", "--shard", "global"]])
 def test_bench_sharded_two_ranks_one_gpu(extra):
     """bench.py's multi-GPU path in 2 fresh processes sharing the GPU (a rehearsal of the
     driver's torchrun launch; times are not a measurement): the gathered P passes checkData."""
@@ -157,9 +158,11 @@ def test_bench_sharded_two_ranks_one_gpu(extra):
     assert out["n_gpus"] == 2 and out["checkData_errors_gathered_P"] == 0
     sh = out["shards"]
     assert sum(sh["entries"]) == out["config"]["nnz"]
-    if out["config"].get("shard_mode") == "local":  # C2 default: the two stacked copies
-        assert sh["rows"] == [out["config"]["M"] // 2] * 2
-        assert sh["entries"][0] == sh["entries"][1]
+    if out["config"].get("shard_mode") == "local":  # contiguous original row panels
+        assert sum(sh["rows"]) == out["config"]["M"] and min(sh["rows"]) > 0
+        if "C2" in extra:  # exactly the two stacked copies
+            assert sh["rows"] == [out["config"]["M"] // 2] * 2
+            assert sh["entries"][0] == sh["entries"][1]
     else:
         assert sum(sh["panels"]) == out["config"]["num_row_panels"]
         assert min(sh["panels"]) > 0
