@@ -703,10 +703,11 @@ def main_sharded_local(args, rank, world):
     rp_loc = (rp64[r0:r1 + 1] - e0).astype(np.uint32)
     ci_loc = np.ascontiguousarray(np.asarray(ci)[e0:e1], dtype=np.uint32)
     t0 = time.perf_counter()
-    plan = Plan(max(r1 - r0, 1), N, rp_loc if r1 > r0 else np.zeros(2, np.uint32), ci_loc,
-                alpha=args.alpha, delta=args.delta, layout=args.layout)
+    # (a panel without stored entries, possible only when nnz < world, has nothing to plan)
+    plan = (Plan(r1 - r0, N, rp_loc, ci_loc, alpha=args.alpha, delta=args.delta,
+                 layout=args.layout) if e1 > e0 else None)
     plan_s = time.perf_counter() - t0
-    st = plan.stats()
+    st = plan.stats() if plan else None
 
     tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
     # A partitioned: the makeData stream is a function of the row, so every rank derives its own
@@ -730,7 +731,7 @@ def main_sharded_local(args, rank, world):
     sp = stream.cuda_stream
 
     def step():
-        if e1 > e0:
+        if plan:
             plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP_loc.data_ptr(), stream=sp, dtype=dtype)
 
     for _ in range(args.warmup):
@@ -759,7 +760,7 @@ def main_sharded_local(args, rank, world):
     tg = time.perf_counter()
     P = D.gather_p(dP, 0)  # sum-reduce: each output written by exactly one rank
     gather_ms = (time.perf_counter() - tg) * 1e3
-    st_after = plan.stats()
+    st_after = plan.stats() if plan else None
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -777,7 +778,7 @@ def main_sharded_local(args, rank, world):
     s = 4 if dtype == F32 else 2
     bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
     achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
-    kern, _ = kernel_name(st, st_after, K, dtype, args.layout)
+    kern = kernel_name(st, st_after, K, dtype, args.layout)[0] if st else "none (empty panel)"
     mean_ms = sum(ms_all) / world
     out = {
         "metric": METRIC,
