@@ -12,6 +12,7 @@ for c in $CFGS; do
         C3) ARGS="--workload cop20k_like --K 256 --dtype f16" ;;
         C4) ARGS="--workload reddit_like --scale 0.5 --K 128 --dtype f32" ;;
         C5u) ARGS="--workload dlmc_like --mask uniform --K 512 --dtype bf16" ;;
+        C5b) ARGS="--workload dlmc_like --mask block --K 512 --dtype bf16" ;;
     esac
     for v in base var base var; do
         if [ $v = var ]; then export BSMR_LIB_PATH=$VAR; else unset BSMR_LIB_PATH; fi
