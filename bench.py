@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4", "C5"],
+                    help="BASELINE.json config (C1 = the OpenMP host path on nips-like K = 32)")
     ap.add_argument("--K", type=int, default=None)
     ap.add_argument("--alpha", type=float, default=0.3)
     ap.add_argument("--delta", type=float, default=0.3)
@@ -74,6 +75,13 @@ def parse():
                          "(rank 0 clusters, row stage broadcast); local = contiguous original row "
                          "panels of S balanced by stored entries, each rank clustering its own "
                          "panel; auto = local (measured faster for C2 and C4: DESIGN.md section 7)")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="run the multi-GPU path (torch.distributed, RCCL) even at world size 1")
+    ap.add_argument("--strong", default="auto", choices=["auto", "on", "off"],
+                    help="strong_C4 block (the north_star reddit row-panel split, both splits, "
+                         "with the global plan's N = 1 point); auto = for C2 at N > 1")
+    ap.add_argument("--strong-scale", type=float, default=1.0,
+                    help="reddit-like size of the strong_C4 block (1 = 232 M stored entries)")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -127,15 +135,7 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     nerr = O.check_data(P[:nnz_s], P_gpu[:nnz_s])
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
+    model = cpu_model()
     full = "full workload" if row_end == M else f"rows [0, {row_end}) of {M}"
     return {
         "value": round(2.0 * nnz_s * K / med / 1e9, 3),
@@ -345,13 +345,21 @@ def pmc_traffic_inrun(args):
 def main():
     args = parse()
     from bsmr import dist as D
+    from bsmr import set_default_tuning, tuning_from_env
 
+    # launch-layout knobs from BSMR_* variables (A/B runs; the library itself reads no
+    # environment), recorded in the line when any is set
+    args.tuning = tuning_from_env()
+    set_default_tuning(args.tuning)
     rank, world, local = D.env_rank_world()
+    if args.config == "C1":
+        return main_c1(args)
+    sharded = world > 1 or args.force_sharded
     # in-run PMC traffic (children, before this process touches the GPU; N=1 only)
-    args.pmc_result = pmc_traffic_inrun(args) if world == 1 else (None, None)
+    args.pmc_result = pmc_traffic_inrun(args) if not sharded else (None, None)
     import torch
 
-    if world > 1:
+    if sharded:
         # one rank per GPU; BSMR_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
         # multi-process path (ranks then share devices; their timings are not a measurement)
         torch.cuda.set_device(local % torch.cuda.device_count())
@@ -359,6 +367,95 @@ def main():
         return main_sharded(args, rank, world)
     torch.cuda.set_device(0)
     return main_single(args)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def main_c1(args):
+    """BASELINE.json C1: nips-like K = 32 fp32 through the OpenMP host path (the product's
+    bsmr_sddmm_cpu, host.cpp:45-76 restated: per stored entry a serial fp32 sum in k order, rows
+    split over all host threads), timed on this box's cores (1 warm-up, median of >= 5 runs),
+    then checkData (checkData.hpp:44-79) of its P against the GPU engine's P on the same
+    operands; the GPU's K = 32 rate on the same plan is reported beside it."""
+    import numpy as np
+    import torch
+
+    from bsmr import Plan, check_data, make_data, sddmm_cpu, synth
+
+    M, N, rp, ci = synth.nips_like()
+    K = args.K or 32
+    nnz = len(ci)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    A = make_data(M * K)
+    B = make_data(N * K)
+    sddmm_cpu(M, N, rp, ci, K, A, B, threads=threads)  # warm-up
+    times = []
+    t_end = time.perf_counter() + 20.0
+    while len(times) < 5 or (time.perf_counter() < t_end and len(times) < 50):
+        t0 = time.perf_counter()
+        P_cpu = sddmm_cpu(M, N, rp, ci, K, A, B, threads=threads)
+        times.append(time.perf_counter() - t0)
+    cpu_ms = statistics.median(times) * 1e3
+    flops = 2.0 * nnz * K
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, device=0, layout=args.layout)
+    dA = torch.from_numpy(A).to(dev)
+    dB = torch.from_numpy(B).to(dev)
+    dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    for _ in range(args.warmup):
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=sp)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    gpu_ms = e0.elapsed_time(e1) / args.steps
+    nerr = check_data(P_cpu, dP.cpu().numpy())
+    st = plan.stats()
+    out = {
+        "metric": METRIC,
+        "value": round(flops / (cpu_ms * 1e-3) / 1e9, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": 0,
+        "steps": len(times),
+        "warmup": 1,
+        "ms_per_step": round(cpu_ms, 4),
+        "higher_is_better": True,
+        "scaling": "none",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "C1: nips_like 1500x12419, 746,316 nnz (Zipf 1.1 columns, seed "
+                               f"20250801), fp32 A/B, K={K}: OpenMP host path + checkData",
+                   "M": M, "N": N, "nnz": nnz, "K": K,
+                   "parallelism": f"host: {threads} threads (bsmr_sddmm_cpu, rows split into "
+                                  "equal-entry ranges)"},
+        "cpu": {"cores": threads, "model": cpu_model(), "kind": "product host SDDMM "
+                "(csrc/host_check.cpp, host.cpp:45-76 loop order, no FMA contraction)",
+                "runs_ms": [round(t * 1e3, 4) for t in times]},
+        "checkData_errors_cpu_vs_gpu": nerr,
+        "gpu_same_workload": {"value": round(flops / (gpu_ms * 1e-3) / 1e9, 2),
+                              "ms_per_step": round(gpu_ms, 5), "steps": args.steps,
+                              "alpha": args.alpha, "delta": args.delta,
+                              "kernel": kernel_name(st, plan.stats(), K, 0, args.layout)[0],
+                              "speedup_over_cpu": round(cpu_ms / gpu_ms, 1)},
+    }
+    print(json.dumps(out), flush=True)
 
 
 def main_single(args):
@@ -460,7 +557,12 @@ def main_single(args):
                 "traffic_source": traffic_src,
                 "hbm_bytes_alg_per_launch": bytes_alg,
                 "note": "algorithmic FLOPs of the tiles computed (the dense-sampled launch "
-                        "computes every product of a non-empty tile)"}
+                        "computes every product of a non-empty tile)",
+                # no credit for zero-padding - the sampled entries' own flops
+                "achieved_sampled_flops": round(flops_rank / (ms_per_step * 1e-3) / 1e12, 3),
+                "frac_sampled_flops": round(flops_rank / (ms_per_step * 1e-3) / 1e12 /
+                                            MFMA_HALF_PEAK_TFS, 5),
+                "frac_hbm": round(achieved / HBM_PEAK_GBS, 4)}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -483,6 +585,7 @@ def main_single(args):
             "plan_build_s": round(plan_s, 3), "row_reorder_ms": round(st["row_reorder_ms"], 3),
             "col_reorder_ms": round(st["col_reorder_ms"], 3),
             "rowblock_layout": {k: st_after[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
+            **({"tuning": args.tuning} if args.tuning else {}),
         },
         "roofline": roof,
         # the launch's dense-tile-only / residual-only halves (None when the layout keeps no
@@ -522,21 +625,76 @@ def sharded_workload(args, world):
                    "permutation, synth.stack_copies), one C2 per GPU", "weak")
 
 
-def main_sharded(args, rank, world):
-    """Row-panel shards over `world` ranks (bsmr/dist.py): of one global plan (--shard global),
-    or contiguous original row panels each planned on its own rank (--shard local)."""
-    mode = "global" if args.shard == "global" else "local"
-    if mode == "local":
-        return main_sharded_local(args, rank, world)
-    import numpy as np
+def _timed_steps(step, steps, warmup, stream):
+    """warmup untimed steps, then `steps` between HIP events on the launch stream, bracketed by a
+    barrier + device synchronisation on both sides; returns this rank's ms per step."""
     import torch
     import torch.distributed as dist
 
-    from bsmr import F32, check_data, make_data, sddmm_cpu
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    return e0.elapsed_time(e1) / max(steps, 1)
+
+
+def _host_ref(M, N, rp, ci, K, A, B, dtype, tdt):
+    """The product's host SDDMM (host.cpp:45-76 restated) on the rounded inputs of the run."""
+    import torch
+
+    from bsmr import F32, sddmm_cpu
+
+    if dtype == F32:
+        Ar, Br = A, B
+    else:
+        Ar = torch.from_numpy(A).to(tdt).float().numpy()
+        Br = torch.from_numpy(B).to(tdt).float().numpy()
+    return sddmm_cpu(M, N, rp, ci, K, Ar, Br,
+                     threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+
+
+def _bcast_b(B_host, N, K, tdt, dev):
+    """B generated on rank 0 and broadcast once over RCCL (xGMI); returns (dB, ms)."""
+    import torch
+    import torch.distributed as dist
+
     from bsmr import dist as D
 
-    dev = torch.device("cuda", torch.cuda.current_device())
-    (M, N, rp, ci), K, dtype, desc, scaling = sharded_workload(args, world)
+    if dist.get_rank() == 0:
+        dB = torch.from_numpy(B_host).to(dev).to(tdt)
+    else:
+        dB = torch.empty(N * K, dtype=tdt, device=dev)
+    dist.barrier()
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
+    D.broadcast_(dB, 0)
+    torch.cuda.synchronize()
+    return dB, (time.perf_counter() - tb) * 1e3
+
+
+def shard_global(args, rank, world, wl, dev, time_whole=False):
+    """Row-panel shards of ONE global BSMR plan (the reference layout): rank 0
+    clusters and broadcasts the row stage over RCCL, every rank rebuilds the column stage, cuts the
+    same contiguous panel ranges, holds only its panels' A rows and runs bsmr_sddmm_panels_local;
+    B broadcast once; P sum-reduced to rank 0. time_whole: rank 0 also times the unsharded
+    whole-plan launch (the N = 1 point of the same plan) before the shards run. Returns the
+    report dict on rank 0 (with the gathered P under "_P"), None elsewhere."""
+    import numpy as np
+    import torch
+
+    from bsmr import make_data
+    from bsmr import dist as D
+
+    (M, N, rp, ci), K, dtype, desc, scaling = wl
     nnz = len(ci)
     plan, pinfo = D.distribute_plan(M, N, rp, ci, dev, alpha=args.alpha, delta=args.delta,
                                     layout=args.layout)
@@ -545,55 +703,44 @@ def main_sharded(args, rank, world):
     p0, p1 = plan.shard(K, rank, world, dtype)  # same cuts on every rank (same global plan)
     cut_s = time.perf_counter() - t0
     rows = plan.array("reorderedRows")
-
     tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
     # A partitioned: the makeData stream is a function of the row, so every rank derives its own
     # panels' rows locally (nothing of A is sent); only they reach this GPU
     A = make_data(M * K)
+    B = make_data(N * K) if rank == 0 else None
+    dB, bcast_ms = _bcast_b(B, N, K, tdt, dev)
+    whole_ms = None
+    if time_whole:  # rank 0: the same plan unsharded, whole A on this GPU
+        if rank == 0:
+            dA_all = torch.from_numpy(A).to(dev).to(tdt)
+            dP1 = torch.zeros(nnz, dtype=torch.float32, device=dev)
+
+            def whole():
+                plan.sddmm(dA_all.data_ptr(), dB.data_ptr(), K, dP1.data_ptr(), stream=sp,
+                           dtype=dtype)
+        else:
+            def whole():
+                pass
+        whole_ms = _timed_steps(whole, args.steps, args.warmup, stream)
+        if rank == 0:
+            del dA_all, dP1
+            torch.cuda.empty_cache()
     A_local = D.shard_a_rows(A, K, rows, p0, p1)
     dA = torch.from_numpy(A_local.reshape(-1)).to(dev).to(tdt)
     if dA.numel() == 0:
         dA = torch.zeros(K, dtype=tdt, device=dev)
-    # B broadcast once from rank 0 over RCCL (xGMI)
-    if rank == 0:
-        B = make_data(N * K)
-        dB = torch.from_numpy(B).to(dev).to(tdt)
-    else:
-        B = None
-        dB = torch.empty(N * K, dtype=tdt, device=dev)
-    dist.barrier()
-    torch.cuda.synchronize()
-    tb = time.perf_counter()
-    D.broadcast_(dB, 0)
-    torch.cuda.synchronize()
-    bcast_ms = (time.perf_counter() - tb) * 1e3
     dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
 
     def step():
-        plan.sddmm_panels_local(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), p0, p1,
-                                stream=sp, dtype=dtype)
+        if p1 > p0:
+            plan.sddmm_panels_local(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), p0, p1,
+                                    stream=sp, dtype=dtype)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(args.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    dist.barrier()
-    ms_mine = e0.elapsed_time(e1) / args.steps
+    ms_mine = _timed_steps(step, args.steps, args.warmup, stream)
     ms_all = D.all_values(ms_mine, dev)
-    ms_per_step = max(ms_all)  # whole-job time = slowest rank
-
-    # this rank's share: stored entries of its panels
-    lens = np.diff(rp.astype(np.int64))
+    lens = np.diff(np.asarray(rp, dtype=np.int64))
     mine = int(lens[rows[16 * p0:min(16 * p1, len(rows))]].sum())
     entries_all = D.all_values(mine, dev)
     panels_all = D.all_values(p1 - p0, dev)
@@ -603,99 +750,61 @@ def main_sharded(args, rank, world):
     gather_ms = (time.perf_counter() - tg) * 1e3
     st_after = plan.stats()
     if rank != 0:
-        dist.destroy_process_group()
-        return
-    # checkData of the assembled P against the product's host SDDMM (host.cpp:45-76)
-    if dtype == F32:
-        Ar, Br = A, B
-    else:
-        Ar = torch.from_numpy(A).to(tdt).float().numpy()
-        Br = dB.float().cpu().numpy()
-    ref = sddmm_cpu(M, N, rp, ci, K, Ar, Br,
-                    threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
-    nerr = check_data(ref, P)
-
-    flops = 2.0 * nnz * K
-    value = flops / (ms_per_step * 1e-3) / 1e9
-    s = 4 if dtype == F32 else 2
-    bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
-    achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
+        return None
     kern, _ = kernel_name(st, st_after, K, dtype, args.layout)
-    mean_ms = sum(ms_all) / world
+    ms = max(ms_all)
     out = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "GFLOP/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
-        "higher_is_better": True,
-        "scaling": scaling,
-        "vs_baseline": None,
-        "dtype": {0: "f32", 1: "f16", 2: "bf16"}[dtype],
-        "data": "synthetic",
-        "config": {
-            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}",
-            "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
-            "parallelism": (f"row-panel shards x{world} of one global BSMR plan (rank 0 clusters, "
-                            "row stage broadcast over RCCL, column stage rebuilt per rank), A "
-                            "rows local to their shard, B broadcast once (RCCL), P sum-reduced "
-                            "to rank 0"),
-            "shard_mode": "global",
-            "backend": dist.get_backend(),
-            "num_clusters": st["num_clusters"], "num_row_panels": st["num_row_panels"],
-            "plan_build_s": round(pinfo["plan_build_s"], 3),
-            "row_reorder_ms": round(st["row_reorder_ms"], 3),
-            "plan_distribution_ms": round(pinfo["distribute_ms"], 3),
-            "row_stage_bcast_ms": round(pinfo["row_stage_bcast_ms"], 3),
-            "row_stage_bytes": pinfo["row_stage_bytes"],
-            "shard_cut_s": round(cut_s, 3),
-            "b_broadcast_ms": round(bcast_ms, 3),
-            "p_gather_ms": round(gather_ms, 3),
-        },
+        "split": "global",
+        "parallelism": (f"row-panel shards x{world} of one global BSMR plan (rank 0 clusters, row "
+                        "stage broadcast over RCCL, column stage rebuilt per rank), A rows local "
+                        "to their shard, B broadcast once (RCCL), P sum-reduced to rank 0"),
+        "ms_per_step": round(ms, 5),
+        "value": round(2.0 * nnz * K / (ms * 1e-3) / 1e9, 2),
+        "num_clusters": st["num_clusters"], "num_row_panels": st["num_row_panels"],
+        "plan_build_s": round(pinfo["plan_build_s"], 3),
+        "row_reorder_ms": round(st["row_reorder_ms"], 3),
+        "plan_distribution_ms": round(pinfo["distribute_ms"], 3),
+        "row_stage_bcast_ms": round(pinfo["row_stage_bcast_ms"], 3),
+        "row_stage_bytes": pinfo["row_stage_bytes"],
+        "shard_cut_s": round(cut_s, 3),
+        "b_broadcast_ms": round(bcast_ms, 3),
+        "p_gather_ms": round(gather_ms, 3),
         "shards": {
             "panels": [int(x) for x in panels_all],
             "entries": [int(x) for x in entries_all],
             "ms_per_step": [round(x, 5) for x in ms_all],
-            "imbalance_max_over_mean": round(ms_per_step / mean_ms, 3),
+            "imbalance_max_over_mean": round(ms / (sum(ms_all) / world), 3),
             "kernel": "bsmr_sddmm_panels_local -> " + kern,
         },
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
-                     "frac": round(achieved / (HBM_PEAK_GBS * world), 4), "traffic": None,
-                     "kernel": kern, "bytes_alg_per_launch": bytes_alg,
-                     "note": "whole-job algorithmic bytes per step over the slowest rank's time, "
-                             "against world x 8 TB/s"},
-        "checkData_errors_gathered_P": nerr,
+        "_P": P,
     }
-    print(json.dumps(out), flush=True)
-    dist.destroy_process_group()
+    if whole_ms is not None:
+        out["whole_plan_one_gpu"] = {
+            "ms_per_step": round(whole_ms, 5),
+            "value": round(2.0 * nnz * K / (whole_ms * 1e-3) / 1e9, 2),
+            "note": "rank 0 alone, the same global plan unsharded (bsmr_sddmm), timed in this run",
+            "speedup_of_split": round(whole_ms / ms, 3),
+            "strong_scaling_efficiency": round(whole_ms / ms / world, 3)}
+    return out
 
 
-def main_sharded_local(args, rank, world):
+def shard_local(args, rank, world, wl, dev):
     """S cut into `world` contiguous original row panels of equal stored entries; rank r clusters
     and lays out its own panel (a local BSMR plan over rows [r0, r1)), stages only those A rows,
-    receives B once over RCCL and writes P[rowptr[r0]:rowptr[r1]] (contiguous CSR positions), so P
-    assembles by a sum-reduce. No plan crosses ranks, and every rank clusters only its own rows.
-    C4 (reddit-like x1, 8 shards timed alone on one GPU): slowest shard 0.600 ms, imbalance 1.02,
-    against 0.726 ms / 1.19 for shards of the global plan, whose leading panels hold the sparse
-    low-dispersion rows (profiles/r02c/c4_shards/). For the C2 weak-scaling copies the panels are
-    exactly the copies: a shard of one global plan instead interleaves the copies' clusters (the
-    BSMR cluster order follows dispersion, which the copies share), so its row blocks mix unrelated
-    column sets
-    (tools/shard_sim.py --copies N --local, each shard timed alone on one GPU: slowest shard at
-    N = 2 / 4 / 8 local 11.5 / 11.4 / 11.8 us, global 11.7 / 13.4 / 13.5 us; one C2 11.2 us;
-    profiles/r02c/weak_scaling/)."""
+    receives B once over RCCL and writes P[rowptr[r0]:rowptr[r1]] (contiguous CSR positions),
+    gathered to rank 0 segment by segment. No plan crosses ranks. Returns the report dict on
+    rank 0 (gathered P under "_P"), None elsewhere.
+    One-GPU rehearsal (tools/shard_sim.py, each shard timed alone): reddit-like x1, 8 shards:
+    slowest 0.600 ms, imbalance 1.02 (global-plan shards: 0.726 ms, 1.19); C2 weak-scaling
+    copies at N = 2 / 4 / 8: 11.5 / 11.4 / 11.8 us (global 11.7 / 13.4 / 13.5 us), one C2 11.2 us
+    (profiles/r02c/c4_shards/, profiles/r02c/weak_scaling/)."""
     import numpy as np
     import torch
-    import torch.distributed as dist
 
-    from bsmr import F32, Plan, check_data, make_data, sddmm_cpu
+    from bsmr import Plan, make_data, sddmm_cpu
     from bsmr import dist as D
 
-    dev = torch.device("cuda", torch.cuda.current_device())
-    (M, N, rp, ci), K, dtype, desc, scaling = sharded_workload(args, world)
+    (M, N, rp, ci), K, dtype, desc, scaling = wl
     nnz = len(ci)
     rp64 = np.asarray(rp, dtype=np.int64)
     r0, r1 = D.row_range_cut(rp64, rank, world)
@@ -703,29 +812,19 @@ def main_sharded_local(args, rank, world):
     rp_loc = (rp64[r0:r1 + 1] - e0).astype(np.uint32)
     ci_loc = np.ascontiguousarray(np.asarray(ci)[e0:e1], dtype=np.uint32)
     t0 = time.perf_counter()
-    # (a panel without stored entries, possible only when nnz < world, has nothing to plan)
+    # bsmr_plan_create needs >= 2 stored entries: a panel with fewer (only when nnz < 2 world)
+    # has no launch; its one entry, if any, is computed by the product's host SDDMM below
     plan = (Plan(r1 - r0, N, rp_loc, ci_loc, alpha=args.alpha, delta=args.delta,
-                 layout=args.layout) if e1 > e0 else None)
+                 layout=args.layout) if e1 - e0 >= 2 else None)
     plan_s = time.perf_counter() - t0
     st = plan.stats() if plan else None
-
     tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
     # A partitioned: the makeData stream is a function of the row, so every rank derives its own
     # rows locally (nothing of A is sent)
     A = make_data(M * K)
+    B = make_data(N * K) if rank == 0 else None
     dA = torch.from_numpy(np.ascontiguousarray(A[r0 * K:max(r1, r0 + 1) * K])).to(dev).to(tdt)
-    if rank == 0:
-        B = make_data(N * K)
-        dB = torch.from_numpy(B).to(dev).to(tdt)
-    else:
-        B = None
-        dB = torch.empty(N * K, dtype=tdt, device=dev)
-    dist.barrier()
-    torch.cuda.synchronize()
-    tb = time.perf_counter()
-    D.broadcast_(dB, 0)
-    torch.cuda.synchronize()
-    bcast_ms = (time.perf_counter() - tb) * 1e3
+    dB, bcast_ms = _bcast_b(B, N, K, tdt, dev)
     dP_loc = torch.zeros(max(e1 - e0, 1), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
@@ -734,93 +833,173 @@ def main_sharded_local(args, rank, world):
         if plan:
             plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP_loc.data_ptr(), stream=sp, dtype=dtype)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    e_0 = torch.cuda.Event(enable_timing=True)
-    e_1 = torch.cuda.Event(enable_timing=True)
-    e_0.record(stream)
-    for _ in range(args.steps):
-        step()
-    e_1.record(stream)
-    torch.cuda.synchronize()
-    dist.barrier()
-    ms_mine = e_0.elapsed_time(e_1) / args.steps
+    ms_mine = _timed_steps(step, args.steps, args.warmup, stream)
+    if plan is None and e1 - e0 == 1:
+        Ah = dA.float().cpu().numpy().reshape(-1)
+        Bh = dB.float().cpu().numpy()
+        dP_loc[0] = float(sddmm_cpu(r1 - r0, N, rp_loc, ci_loc, K, Ah, Bh)[0])
     ms_all = D.all_values(ms_mine, dev)
-    ms_per_step = max(ms_all)  # whole-job time = slowest rank
     entries_all = D.all_values(e1 - e0, dev)
     rows_all = D.all_values(r1 - r0, dev)
     plan_all = D.all_values(plan_s, dev)
-    dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
-    if e1 > e0:
-        dP[e0:e1] = dP_loc[:e1 - e0]
     torch.cuda.synchronize()
     tg = time.perf_counter()
-    P = D.gather_p(dP, 0)  # sum-reduce: each output written by exactly one rank
+    P = D.gather_segments(dP_loc, e0, e1, nnz, 0)
     gather_ms = (time.perf_counter() - tg) * 1e3
     st_after = plan.stats() if plan else None
     if rank != 0:
+        return None
+    kern = kernel_name(st, st_after, K, dtype, args.layout)[0] if st else "none (empty panel)"
+    ms = max(ms_all)
+    return {
+        "split": "local",
+        "parallelism": (f"row-panel shards x{world} of S in original row order (contiguous "
+                        "panels of equal stored entries), each rank's BSMR plan built on its own "
+                        "panel, A rows local, B broadcast once (RCCL), P segments gathered to "
+                        "rank 0"),
+        "ms_per_step": round(ms, 5),
+        "value": round(2.0 * nnz * K / (ms * 1e-3) / 1e9, 2),
+        "plan_build_s_max": round(max(plan_all), 3),
+        "b_broadcast_ms": round(bcast_ms, 3),
+        "p_gather_ms": round(gather_ms, 3),
+        "shards": {
+            "rows": [int(x) for x in rows_all],
+            "entries": [int(x) for x in entries_all],
+            "ms_per_step": [round(x, 5) for x in ms_all],
+            "imbalance_max_over_mean": round(ms / (sum(ms_all) / world), 3),
+            "kernel": "bsmr_sddmm (rank-local plan) -> " + kern,
+        },
+        "_P": P,
+    }
+
+
+def strong_c4(args, rank, world, dev):
+    """The north_star multi-GPU config (BASELINE.json C4): reddit-like Chung-Lu graph at
+    --strong-scale (232 M stored entries at 1), fp32 K = 128, row-panel sharded over the run's
+    ranks in both splits: the global plan (reference layout; rank 0 also times
+    the unsharded plan = the N = 1 point) and the local one. The pattern is generated on rank 0 and
+    broadcast over RCCL. Both gathered P are checked against the product host SDDMM."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from bsmr import F32, check_data, make_data, synth
+    from bsmr import dist as D
+
+    t0 = time.perf_counter()
+    n = max(1024, int(232965 * args.strong_scale))
+    if rank == 0:
+        M, N, rp, ci = synth.reddit_like(args.strong_scale)
+        lens = torch.tensor([M, len(ci)], dtype=torch.int64, device=dev)
+    else:
+        lens = torch.zeros(2, dtype=torch.int64, device=dev)
+    D.broadcast_(lens, 0)
+    M, nnz = int(lens[0]), int(lens[1])
+    assert M == n
+    d_rp = (torch.from_numpy(rp.view(np.int32)).to(dev) if rank == 0
+            else torch.empty(M + 1, dtype=torch.int32, device=dev))
+    d_ci = (torch.from_numpy(ci.view(np.int32)).to(dev) if rank == 0
+            else torch.empty(nnz, dtype=torch.int32, device=dev))
+    D.broadcast_(d_rp, 0)
+    D.broadcast_(d_ci, 0)
+    rp = d_rp.cpu().numpy().view(np.uint32)
+    ci = d_ci.cpu().numpy().view(np.uint32)
+    del d_rp, d_ci
+    gen_s = time.perf_counter() - t0
+    K, dtype = 128, F32
+    desc = (f"C4: reddit_like Chung-Lu power law x{args.strong_scale} (seed 20250803), "
+            f"{M}^2, {nnz:,} stored entries, fp32 A/B, K={K}")
+    wl = ((M, M, rp, ci), K, dtype, desc, "strong")
+    res = {}
+    for split in ("global", "local"):
+        try:
+            if split == "global":
+                r = shard_global(args, rank, world, wl, dev, time_whole=True)
+            else:
+                r = shard_local(args, rank, world, wl, dev)
+        except Exception as e:  # noqa: BLE001 - reported in the line; the C2 value still prints
+            r = {"error": f"{type(e).__name__}: {e}"[:400]} if rank == 0 else None
+        torch.cuda.empty_cache()
+        res[split] = r
+        dist.barrier()
+    if rank != 0:
+        return None
+    ref = _host_ref(M, M, rp, ci, K, make_data(M * K), make_data(M * K), dtype, torch.float32)
+    for split in ("global", "local"):
+        r = res[split]
+        if r is not None and "_P" in r:
+            r["checkData_errors_gathered_P"] = check_data(ref, r.pop("_P"))
+    flops = 2.0 * nnz * K
+    return {"workload": desc, "M": M, "nnz": nnz, "K": K, "n_gpus": world,
+            "flops_per_step": flops, "pattern_gen_and_bcast_s": round(gen_s, 2),
+            "global": res["global"], "local": res["local"],
+            "note": "strong scaling of the one matrix; value = 2 nnz K / slowest rank's ms; "
+                    "whole_plan_one_gpu (global) is the N = 1 point measured in the same run"}
+
+
+def main_sharded(args, rank, world):
+    """Multi-GPU line: the config's row-panel split (--shard; C2 = weak scaling over stacked
+    copies, the line's `value`), plus for C2 at N > 1 (or --strong on) the north_star reddit
+    split (strong_C4 block: both splits, the N = 1 point of the global plan, per-rank ms,
+    imbalance, broadcast and plan times)."""
+    import torch
+    import torch.distributed as dist
+
+    from bsmr import check_data
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    wl = sharded_workload(args, world)
+    (M, N, rp, ci), K, dtype, desc, scaling = wl
+    mode = "global" if args.shard == "global" else "local"
+    r = (shard_global(args, rank, world, wl, dev) if mode == "global"
+         else shard_local(args, rank, world, wl, dev))
+    do_strong = args.strong == "on" or (args.strong == "auto" and world > 1 and args.config == "C2")
+    strong = strong_c4(args, rank, world, dev) if do_strong else None
+    if rank != 0:
         dist.destroy_process_group()
         return
-    if dtype == F32:
-        Ar, Br = A, B
-    else:
-        Ar = torch.from_numpy(A).to(tdt).float().numpy()
-        Br = dB.float().cpu().numpy()
-    ref = sddmm_cpu(M, N, rp, ci, K, Ar, Br,
-                    threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
-    nerr = check_data(ref, P)
-
-    flops = 2.0 * nnz * K
-    value = flops / (ms_per_step * 1e-3) / 1e9
-    s = 4 if dtype == F32 else 2
+    tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
+    from bsmr import make_data
+    ref = _host_ref(M, N, rp, ci, K, make_data(M * K), make_data(N * K), dtype, tdt)
+    nerr = check_data(ref, r.pop("_P"))
+    nnz = len(ci)
+    ms = r["ms_per_step"]
+    s = 4 if dtype == 0 else 2
     bytes_alg = s * K * (M + N) + 4.0 * nnz + 4.0 * (M + 1) + 4.0 * nnz
-    achieved = bytes_alg / (ms_per_step * 1e-3) / 1e9
-    kern = kernel_name(st, st_after, K, dtype, args.layout)[0] if st else "none (empty panel)"
-    mean_ms = sum(ms_all) / world
+    achieved = bytes_alg / (ms * 1e-3) / 1e9
+    cfg = {"workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}",
+           "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
+           "parallelism": r.pop("parallelism"), "shard_mode": mode, "backend": dist.get_backend()}
+    if args.tuning:
+        cfg["tuning"] = args.tuning
+    for k in list(r):
+        if k not in ("split", "ms_per_step", "value", "shards"):
+            cfg[k] = r.pop(k)
     out = {
         "metric": METRIC,
-        "value": round(value, 2),
+        "value": r["value"],
         "unit": "GFLOP/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
+        "ms_per_step": ms,
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": {0: "f32", 1: "f16", 2: "bf16"}[dtype],
         "data": "synthetic",
-        "config": {
-            "workload": desc + f", K={K}, BSMR alpha={args.alpha} delta={args.delta}",
-            "M": M, "N": N, "nnz": nnz, "K": K, "alpha": args.alpha, "delta": args.delta,
-            "parallelism": (f"row-panel shards x{world} of S in original row order (contiguous "
-                            "panels of equal stored entries), each rank's BSMR plan built on its "
-                            "own panel, A rows local, B broadcast once (RCCL), P sum-reduced to "
-                            "rank 0"),
-            "shard_mode": "local",
-            "backend": dist.get_backend(),
-            "plan_build_s_max": round(max(plan_all), 3),
-            "b_broadcast_ms": round(bcast_ms, 3),
-            "p_gather_ms": round(gather_ms, 3),
-        },
-        "shards": {
-            "rows": [int(x) for x in rows_all],
-            "entries": [int(x) for x in entries_all],
-            "ms_per_step": [round(x, 5) for x in ms_all],
-            "imbalance_max_over_mean": round(ms_per_step / mean_ms, 3),
-            "kernel": "bsmr_sddmm (rank-local plan) -> " + kern,
-        },
+        "config": cfg,
+        "shards": r["shards"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                      "frac": round(achieved / (HBM_PEAK_GBS * world), 4), "traffic": None,
-                     "kernel": kern, "bytes_alg_per_launch": bytes_alg,
+                     "kernel": r["shards"]["kernel"], "bytes_alg_per_launch": bytes_alg,
                      "note": "whole-job algorithmic bytes per step over the slowest rank's time, "
                              "against world x 8 TB/s"},
         "checkData_errors_gathered_P": nerr,
     }
+    if strong is not None:
+        out["strong_C4"] = strong
     print(json.dumps(out), flush=True)
     dist.destroy_process_group()
 

@@ -22,9 +22,10 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 5  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 6  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
-                              bsmr_sddmm_panels_local, host SDDMM + checkData */
+                              bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
+                              the plan options (no environment reads in the library) */
 
 typedef enum {
     BSMR_OK = 0,
@@ -75,6 +76,40 @@ void bsmr_make_data(uint64_t n, float* out);
 /* ------------------------------------------------------------------------ the plan ---- */
 typedef struct bsmr_plan bsmr_plan;
 
+/* Launch-layout tuning knobs of the SDDMM engine (measurement, A/B experiments, tests). Every
+ * field's "auto" value (-1, or < 0 for the floats; diag 0) keeps the measured default. Results
+ * are identical for every setting (checkData tolerance) except `diag`, whose profiling ablations
+ * drop work on purpose. The library never reads the environment: a caller that wants the
+ * BSMR_<FIELD> variables (the tools/ A/B scripts) copies them in with bsmr_tuning_from_env. */
+typedef struct {
+    uint32_t diag;             /* BSMR_DIAG ablation bits (sddmm.hip; results WRONG); 0 = off */
+    int32_t piece_order;       /* BSMR_PIECE_ORDER: 1 = column order inside an item; -1 = 0 */
+    int32_t tile_min_f32;      /* BSMR_TILE_MIN_F32: fp32 tiles with fewer entries run as residual
+                                  entries on the row-block launch; -1 = 257 (all demoted) */
+    int32_t tile_min_half;     /* BSMR_TILE_MIN_HALF: the same for fp16/bf16; -1 = 128 */
+    int32_t piece_max;         /* BSMR_PIECE_MAX: entries per column-run piece, 1..16; -1 = 16 */
+    float piece_weight;        /* BSMR_PIECE_WEIGHT: item cost of a piece in entries; < 0 = 4 */
+    float shard_piece_weight;  /* BSMR_SHARD_PIECE_WEIGHT: the same for shard cuts; < 0 = 4 */
+    float dense_min;           /* BSMR_DENSE_MIN: density from which fp16/bf16 patterns take the
+                                  dense-sampled launch; < 0 = 0.05 */
+    int32_t orig_rows;         /* BSMR_ORIG_ROWS: original-order row blocks 0 never, 1 always,
+                                  -1 auto */
+    int32_t orig_contig;       /* BSMR_ORIG_CONTIG: their XCD deal, 0 round robin, 1 contiguous
+                                  eighths; -1 = 1 */
+    int32_t dense_ks;          /* BSMR_DENSE_KS: dense-sampled waves per tile, 1 = four, 2 = eight,
+                                  0 = by tile count; -1 = 0 */
+    int32_t dense_ns;          /* BSMR_DENSE_NS: dense-sampled LDS stages 2..5; -1 = 2 */
+    int32_t out_staged;        /* BSMR_OUT_STAGED: results through LDS in CSR order, 0 never,
+                                  1 always, -1 auto (P > 8 MiB) */
+    int32_t l2_range_kb;       /* BSMR_L2_RANGE_KB: B bytes per XCD column range (>= 64);
+                                  -1 = auto */
+} bsmr_tuning;
+
+void bsmr_tuning_default(bsmr_tuning* t);
+/* Debug helper: overwrite the fields whose BSMR_<FIELD> environment variable is set (names in
+ * the comments above). Returns the number of fields taken from the environment. */
+int bsmr_tuning_from_env(bsmr_tuning* t);
+
 typedef struct {
     float alpha;              /* similarity threshold  (Options -a, default 0.3) */
     float delta;              /* tile density threshold (Options -d, default 0.3) */
@@ -84,6 +119,7 @@ typedef struct {
     int exact_similarity;     /* !=0: evaluate every similarity with the exact fp32 tree */
     int layout;               /* SDDMM launch layout: BSMR_LAYOUT_AUTO / _ROWBLOCK / _COLMAJOR */
     uint32_t lds_budget_kb;   /* LDS per row-block workgroup, 16..160 KiB; 0 = default (144) */
+    const bsmr_tuning* tuning;  /* launch-layout knobs (copied at plan creation); NULL = auto */
 } bsmr_plan_options;
 
 /* AUTO: A rows staged in LDS per row block for rows of 256 B .. 2 KiB (fp32 K = 64..512,

@@ -37,11 +37,25 @@ class BsmrError(RuntimeError):
     pass
 
 
+class Tuning(C.Structure):
+    """bsmr_tuning: launch-layout knobs (include/bsmr.h). "auto" = -1 (diag 0)."""
+    _fields_ = [("diag", C.c_uint32), ("piece_order", C.c_int32), ("tile_min_f32", C.c_int32),
+                ("tile_min_half", C.c_int32), ("piece_max", C.c_int32),
+                ("piece_weight", C.c_float), ("shard_piece_weight", C.c_float),
+                ("dense_min", C.c_float), ("orig_rows", C.c_int32), ("orig_contig", C.c_int32),
+                ("dense_ks", C.c_int32), ("dense_ns", C.c_int32), ("out_staged", C.c_int32),
+                ("l2_range_kb", C.c_int32)]
+
+
+# tuning field <- its debug environment variable (bsmr_tuning_from_env)
+TUNING_ENV = {f: "BSMR_" + f.upper() for f, _ in Tuning._fields_}
+
+
 class PlanOptions(C.Structure):
     _fields_ = [("alpha", C.c_float), ("delta", C.c_float), ("free_mem_bytes", C.c_uint64),
                 ("device", C.c_int), ("cluster_batch", C.c_uint32),
                 ("exact_similarity", C.c_int), ("layout", C.c_int),
-                ("lds_budget_kb", C.c_uint32)]
+                ("lds_budget_kb", C.c_uint32), ("tuning", C.POINTER(Tuning))]
 
 
 LAYOUTS = {"auto": 0, "rowblock": 1, "colmajor": 2}
@@ -101,14 +115,15 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 5  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 6  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
     "bsmr_last_error", "bsmr_abi_version", "bsmr_csr_load_mtx", "bsmr_csr_load_smtx",
     "bsmr_csr_load_snap", "bsmr_csr_load", "bsmr_csr_create",
     "bsmr_csr_info", "bsmr_csr_rowptr", "bsmr_csr_colidx", "bsmr_csr_values", "bsmr_csr_free",
-    "bsmr_make_data", "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
+    "bsmr_make_data", "bsmr_tuning_default", "bsmr_tuning_from_env",
+    "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
     "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
     "bsmr_sddmm", "bsmr_sddmm_batch", "bsmr_plan_shard", "bsmr_plan_shard_dtype",
     "bsmr_shard_cuts", "bsmr_sddmm_panels", "bsmr_sddmm_panels_local",
@@ -154,6 +169,9 @@ def lib():
     L.bsmr_csr_free.argtypes = [vp]
     L.bsmr_make_data.argtypes = [C.c_uint64, _f32p]
     L.bsmr_plan_options_default.argtypes = [C.POINTER(PlanOptions)]
+    L.bsmr_tuning_default.argtypes = [C.POINTER(Tuning)]
+    L.bsmr_tuning_from_env.argtypes = [C.POINTER(Tuning)]
+    L.bsmr_tuning_from_env.restype = C.c_int
     L.bsmr_plan_create.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_uint32,
                                    C.POINTER(PlanOptions), C.POINTER(vp)]
     L.bsmr_plan_recolumn.argtypes = [vp, C.c_float]
@@ -192,6 +210,50 @@ def _check(status, what):
     if status != 0:
         msg = lib().bsmr_last_error().decode(errors="replace")
         raise BsmrError(f"{what} failed with status {status}: {msg}")
+
+
+_default_tuning = {}
+
+
+def tuning_from_env(env=None):
+    """The tuning knobs given as BSMR_<FIELD> variables, as a {field: value} dict for Plan(tuning=).
+    env: a mapping (e.g. a test's parameters); None reads this process's environment through the
+    library's own parser (bsmr_tuning_from_env). The library never reads them by itself."""
+    t = Tuning()
+    lib().bsmr_tuning_default(C.byref(t))
+    base = {f: getattr(t, f) for f, _ in Tuning._fields_}
+    if env is None:
+        lib().bsmr_tuning_from_env(C.byref(t))
+        return {f: getattr(t, f) for f, _ in Tuning._fields_ if getattr(t, f) != base[f]}
+    out = {}
+    for f, _ in Tuning._fields_:
+        v = env.get(TUNING_ENV[f])
+        if v is None:
+            continue
+        if f in ("orig_rows", "out_staged"):  # tri-state: "0" never, "1" always, else auto
+            out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
+        elif f in ("piece_weight", "shard_piece_weight", "dense_min"):
+            out[f] = float(v)
+        else:
+            out[f] = int(v)
+    return out
+
+
+def set_default_tuning(tuning):
+    """Tuning applied to every later Plan built without an explicit `tuning` (tools and bench
+    call this with tuning_from_env() so their A/B runs can be steered from the environment)."""
+    global _default_tuning
+    _default_tuning = dict(tuning or {})
+
+
+def _tuning_struct(tuning):
+    t = Tuning()
+    lib().bsmr_tuning_default(C.byref(t))
+    for k, v in (tuning or {}).items():
+        if k not in TUNING_ENV:
+            raise BsmrError(f"unknown tuning field {k!r}")
+        setattr(t, k, v)
+    return t
 
 
 def make_data(n):
@@ -267,7 +329,8 @@ class Plan:
 
     def __init__(self, M, N, rowptr, colidx, alpha=0.3, delta=0.3, free_mem_bytes=0, device=0,
                  cluster_batch=0, exact_similarity=False, layout="auto", lds_budget_kb=0,
-                 _row_stage=None):
+                 tuning=None, _row_stage=None):
+        """tuning: {bsmr_tuning field: value} (None = the process default, normally empty)."""
         rowptr = np.ascontiguousarray(rowptr, np.uint32)
         colidx = np.ascontiguousarray(colidx, np.uint32)
         o = PlanOptions()
@@ -280,6 +343,8 @@ class Plan:
         o.exact_similarity = 1 if exact_similarity else 0
         o.layout = LAYOUTS[layout]
         o.lds_budget_kb = int(lds_budget_kb)
+        self._tuning = _tuning_struct(_default_tuning if tuning is None else tuning)
+        o.tuning = C.pointer(self._tuning)
         self.M, self.N, self.nnz = int(M), int(N), int(len(colidx))
         h = C.c_void_p()
         if _row_stage is None:
@@ -293,7 +358,7 @@ class Plan:
 
     @classmethod
     def from_row_stage(cls, rowptr, colidx, hdr, rows, delta=0.3, device=0, layout="auto",
-                       lds_budget_kb=0):
+                       lds_budget_kb=0, tuning=None):
         """bsmr_plan_import_rows: the plan of an exported row stage (no clustering). rows: a
         uint32 numpy array, or an int device pointer (e.g. a broadcast tensor's data_ptr())."""
         if isinstance(rows, np.ndarray):
@@ -302,7 +367,8 @@ class Plan:
         else:
             ptr = int(rows)
         return cls(hdr.M, hdr.N, rowptr, colidx, alpha=hdr.alpha, delta=delta, device=device,
-                   layout=layout, lds_budget_kb=lds_budget_kb, _row_stage=(hdr, ptr))
+                   layout=layout, lds_budget_kb=lds_budget_kb, tuning=tuning,
+                   _row_stage=(hdr, ptr))
 
     def export_rows(self, rows_out=None):
         """bsmr_plan_export_rows: (header, rows). rows_out: None (a numpy array is returned) or

@@ -8,16 +8,19 @@ split built here:
 1. **Global plan, clustered once.** A bit-exact permutation needs the global first-fit over all
    rows, so rank 0 builds the plan (``bsmr_plan_create``) and broadcasts its row stage (the
    ``bsmr_row_stage`` header and the reordered rows, u32 on the device) over RCCL. The other
-   ranks rebuild the column stage from it (``bsmr_plan_import_rows``): clustering is >99 % of the
-   plan time (reddit_like x1: 85.8 s of 86 s), the column stage a deterministic O(nnz) pass
-   (0.14 s) that is cheaper to recompute than to ship (its arrays are ~12 B per entry).
+   ranks rebuild the column stage from it (``bsmr_plan_import_rows``): clustering is most of the
+   plan time (reddit_like x1 on MI355X: 14.2 s of a 14.5 s plan), the column stage
+   a deterministic O(nnz) pass (0.18 s) that is cheaper to recompute than to ship (its arrays are
+   ~12 B per entry, ~2.8 GB for reddit_like x1, against 0.9 MB of row stage).
 2. **Panel cut.** Every rank holds the same global plan, so every rank computes the same cost-model
    cuts (``bsmr_plan_shard_dtype``) without talking: contiguous panel ranges [p0, p1).
 3. **A partitioned.** A rank uploads only the A rows of its panels, in reordered order
    (``shard_a_rows``), and runs ``bsmr_sddmm_panels_local`` on them.
 4. **B broadcast once** from rank 0 (RCCL), outside the timed region.
-5. **P gathered** by a sum-reduce to rank 0: each output is written by exactly one rank and the
-   others hold 0 there, so the sum is the value exactly.
+5. **P gathered** to rank 0: the local split gathers each rank's contiguous CSR segment
+   (``gather_segments``, bit-exact); shards of the global plan own scattered rows, so their
+   zero-filled nnz buffers are sum-reduced (``gather_p``: exact up to the sign of a zero output,
+   -0.0 + 0.0 = +0.0).
 
 The timed loop has no collective; the whole-job time is the slowest rank's.
 """
@@ -193,10 +196,38 @@ def shard_a_rows(A, K, reordered_rows, p0, p1):
 
 def gather_p(dP, dst=0):
     """P in CSR order on rank `dst`: every rank wrote only its panels' outputs into a zeroed
-    nnz buffer, so a sum-reduce assembles P exactly (x + 0 = x). Returns the host array on dst,
-    None elsewhere."""
+    nnz buffer, so a sum-reduce assembles P (x + 0 = x; exact except that a -0.0 output comes
+    back as +0.0, which checkData cannot see). Returns the host array on dst, None elsewhere."""
     import torch.distributed as dist
 
     c = _comm(dP)
     dist.reduce(c, dst=dst, op=dist.ReduceOp.SUM)
     return c.cpu().numpy() if dist.get_rank() == dst else None
+
+
+def gather_segments(dP_seg, e0, e1, nnz, dst=0):
+    """P in CSR order on rank `dst` from each rank's contiguous CSR segment [e0, e1) (the local
+    split: a rank's rows are one range of original rows). Bit-exact (no arithmetic), and each
+    rank sends only its segment (padded to the longest). Returns the host array on dst."""
+    import torch
+    import torch.distributed as dist
+
+    w, rank = dist.get_world_size(), dist.get_rank()
+    dev = dP_seg.device
+    bounds = torch.zeros(2 * w, dtype=torch.int64, device=dev)
+    bounds[2 * rank], bounds[2 * rank + 1] = int(e0), int(e1)
+    c = _comm(bounds)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    b = [int(x) for x in c.cpu().tolist()]
+    width = max(max(b[2 * r + 1] - b[2 * r] for r in range(w)), 1)
+    send = torch.zeros(width, dtype=torch.float32, device=dev)
+    send[:e1 - e0] = dP_seg[:e1 - e0]
+    send = _comm(send)
+    bufs = [torch.empty_like(send) for _ in range(w)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst)
+    if rank != dst:
+        return None
+    P = np.zeros(int(nnz), np.float32)
+    for r in range(w):
+        P[b[2 * r]:b[2 * r + 1]] = bufs[r][:b[2 * r + 1] - b[2 * r]].cpu().numpy()
+    return P

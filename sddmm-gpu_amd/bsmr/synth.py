@@ -111,76 +111,80 @@ def nips_like(seed=20250801):
     return random_rows(M, N, lens, seed + 1, zipf=1.1)
 
 
-def banded_fem_like(n, nnz_per_row, seed, band=64):
-    """cop20k_A-like: banded FEM block structure plus a few random long-range couplings."""
+def banded_fem_like(n, nnz_per_row, seed, band=64, target=None):
+    """cop20k_A-like: banded FEM block structure plus a few random long-range couplings.
+    nnz_per_row draws per row (80 % inside the band, 20 % anywhere); duplicates merge, so the
+    pattern holds fewer entries than n * nnz_per_row. target: top the pattern up with further
+    draws of the same mix, then keep a seeded sample of exactly `target` distinct entries."""
     rng = np.random.default_rng(seed)
-    rows, cols = [], []
     k_band = int(nnz_per_row * 0.8)
     k_rand = nnz_per_row - k_band
-    for r0 in range(0, n, 4096):
-        r = np.arange(r0, min(n, r0 + 4096))
-        off = rng.integers(-band, band + 1, size=(len(r), k_band))
+
+    def draw(r, kb, kr):
+        off = rng.integers(-band, band + 1, size=(len(r), kb))
         c = np.clip(r[:, None] + off, 0, n - 1)
-        c2 = rng.integers(0, n, size=(len(r), k_rand))
+        c2 = rng.integers(0, n, size=(len(r), kr))
         cc = np.concatenate([c, c2], axis=1)
-        rr = np.repeat(r, cc.shape[1])
-        rows.append(rr)
-        cols.append(cc.reshape(-1))
-    rows = np.concatenate(rows)
-    cols = np.concatenate(cols)
-    key = np.unique(rows.astype(np.int64) * n + cols)
+        return np.repeat(r, cc.shape[1]).astype(np.int64) * n + cc.reshape(-1)
+
+    keys = [draw(np.arange(r0, min(n, r0 + 4096)), k_band, k_rand) for r0 in range(0, n, 4096)]
+    key = np.unique(np.concatenate(keys))
+    while target is not None and len(key) < target:
+        # one more draw per row of the same 4:1 band / random mix until enough distinct entries
+        r = rng.integers(0, n, size=max(1024, 2 * (target - len(key))))
+        extra = draw(r, 1, 0)
+        rnd = rng.random(len(r)) < k_rand / nnz_per_row
+        extra[rnd] = r[rnd].astype(np.int64) * n + rng.integers(0, n, size=int(rnd.sum()))
+        key = np.unique(np.concatenate([key, extra]))
+    if target is not None and len(key) > target:
+        key = np.sort(rng.choice(key, size=target, replace=False))
     return _csr_from_coo(n, n, key // n, key % n)
 
 
 def cop20k_like(seed=20250802):
-    """C3 stand-in: 121,192 x 121,192 FEM-like pattern, ~21.7 nnz/row (2.62M)."""
-    return banded_fem_like(121192, 22, seed, band=48)
+    """C3 stand-in: 121,192 x 121,192 FEM-like pattern with exactly 2,624,331 stored entries
+    (cop20k_A's full pattern, 21.65 per row)."""
+    return banded_fem_like(121192, 22, seed, band=48, target=2_624_331)
 
 
-def chung_lu(n, nnz_target, seed, exponent=2.2, chunk=20_000_000):
+_synth_lib = None
+
+
+def _synth():
+    """lib/libbsmr_synth.so (synth/chung_lu.cpp): the multi-threaded graph generator."""
+    global _synth_lib
+    if _synth_lib is None:
+        import ctypes as C
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                            "libbsmr_synth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing (run `make -C sddmm-gpu_amd`)")
+        L = C.CDLL(path)
+        u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+        L.bsmr_synth_chung_lu.argtypes = [C.c_uint32, C.c_uint64, C.c_uint64, C.c_double, u32p,
+                                          u32p]
+        _synth_lib = L
+    return _synth_lib
+
+
+def chung_lu(n, nnz_target, seed, exponent=2.2):
     """Symmetric power-law graph (Chung-Lu): endpoints drawn with probability proportional to
-    w_i = (i+1)^(-1/(exponent-1)); self loops dropped, each undirected edge kept once, then both
-    directions stored. Draws continue until nnz_target / 2 distinct edges exist (the heavy rows
-    repeat pairs, so a fixed number of draws falls short), and a seeded sample of exactly that
-    many is kept: the result holds nnz_target stored entries (rounded down to even)."""
-    rng = np.random.default_rng(seed)
-    w = (np.arange(1, n + 1, dtype=np.float64)) ** (-1.0 / (exponent - 1.0))
-    cdf = np.cumsum(w)
-    cdf /= cdf[-1]
-    perm = rng.permutation(n)
-    target = int(nnz_target) // 2
-    edges = np.empty(0, dtype=np.int64)
-    draw, total = int(target * 1.1), 0
-    while True:
-        keys = [edges]
-        drawn = 0
-        while drawn < draw:
-            m = min(chunk, draw - drawn)
-            i = perm[np.searchsorted(cdf, rng.random(m))]
-            j = perm[np.searchsorted(cdf, rng.random(m))]
-            keep = i != j
-            lo = np.minimum(i, j)[keep].astype(np.int64)
-            hi = np.maximum(i, j)[keep].astype(np.int64)
-            keys.append(lo * n + hi)
-            drawn += m
-        total += draw
-        edges = np.unique(np.concatenate(keys))
-        del keys
-        if len(edges) >= target:
-            break
-        # distinct edges per draw fall as the graph fills: ask for the shortfall at the current
-        # yield, plus a margin
-        draw = max(1_000_000, int((target - len(edges)) * 1.5 * total / max(len(edges), 1)))
-    if len(edges) > target:
-        edges = np.sort(rng.choice(edges, size=target, replace=False))
-    lo, hi = edges // n, edges % n
-    del edges
-    key = np.concatenate([lo * n + hi, hi * n + lo])
-    del lo, hi
-    key.sort()
-    rowptr = np.zeros(n + 1, dtype=np.int64)
-    rowptr[1:] = np.bincount(key // n, minlength=n)
-    return n, n, np.cumsum(rowptr).astype(np.uint32), (key % n).astype(np.uint32)
+    w_i = (i+1)^(-1/(exponent-1)) over a seeded relabelling of the nodes; self loops dropped,
+    each undirected edge kept once, then both directions stored with ascending columns per row.
+    Draws continue until nnz_target / 2 distinct edges exist (the heavy rows repeat pairs, so a
+    fixed number of draws falls short), and exactly that many are kept (the smallest seeded
+    hashes): the result holds nnz_target stored entries (rounded down to even). Generated in C++
+    over fixed (seed, round, chunk) random streams (synth/chung_lu.cpp: the same pattern for any
+    thread count; reddit_like x1 in ~10 s instead of ~150 s for the numpy form of round 2)."""
+    nnz = int(nnz_target) // 2 * 2
+    rowptr = np.empty(n + 1, np.uint32)
+    colidx = np.empty(nnz, np.uint32)
+    st = _synth().bsmr_synth_chung_lu(int(n), nnz, int(seed), float(exponent), rowptr, colidx)
+    if st != 0:
+        raise ValueError(f"chung_lu: {n} nodes cannot hold {nnz} stored entries")
+    return n, n, rowptr, colidx
 
 
 def reddit_like(scale=1.0, seed=20250803):

@@ -20,6 +20,56 @@ extern "C" void bsmr_plan_options_default(bsmr_plan_options* o) {
     o->exact_similarity = 0;
     o->layout = BSMR_LAYOUT_AUTO;
     o->lds_budget_kb = 0;
+    o->tuning = nullptr;
+}
+
+extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
+    t->diag = 0;
+    t->piece_order = t->tile_min_f32 = t->tile_min_half = t->piece_max = -1;
+    t->piece_weight = t->shard_piece_weight = t->dense_min = -1.0f;
+    t->orig_rows = t->orig_contig = t->dense_ks = t->dense_ns = t->out_staged = -1;
+    t->l2_range_kb = -1;
+}
+
+extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
+    int n = 0;
+    auto geti = [&](const char* name, int32_t& f) {
+        if (const char* v = std::getenv(name)) {
+            f = std::atoi(v);
+            ++n;
+        }
+    };
+    auto getf = [&](const char* name, float& f) {
+        if (const char* v = std::getenv(name)) {
+            f = static_cast<float>(std::atof(v));
+            ++n;
+        }
+    };
+    // tri-state switches: "0" never, "1" always, anything else auto
+    auto get3 = [&](const char* name, int32_t& f) {
+        if (const char* v = std::getenv(name)) {
+            f = v[0] == '0' ? 0 : v[0] == '1' ? 1 : -1;
+            ++n;
+        }
+    };
+    if (const char* v = std::getenv("BSMR_DIAG")) {
+        t->diag = static_cast<uint32_t>(std::atoi(v));
+        ++n;
+    }
+    geti("BSMR_PIECE_ORDER", t->piece_order);
+    geti("BSMR_TILE_MIN_F32", t->tile_min_f32);
+    geti("BSMR_TILE_MIN_HALF", t->tile_min_half);
+    geti("BSMR_PIECE_MAX", t->piece_max);
+    getf("BSMR_PIECE_WEIGHT", t->piece_weight);
+    getf("BSMR_SHARD_PIECE_WEIGHT", t->shard_piece_weight);
+    getf("BSMR_DENSE_MIN", t->dense_min);
+    get3("BSMR_ORIG_ROWS", t->orig_rows);
+    geti("BSMR_ORIG_CONTIG", t->orig_contig);
+    geti("BSMR_DENSE_KS", t->dense_ks);
+    geti("BSMR_DENSE_NS", t->dense_ns);
+    get3("BSMR_OUT_STAGED", t->out_staged);
+    geti("BSMR_L2_RANGE_KB", t->l2_range_kb);
+    return n;
 }
 
 namespace {
@@ -51,26 +101,24 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         p.rb_lds_kb = o.lds_budget_kb;
         p.rb_lds_user = true;
     }
-    if (const char* dg = std::getenv("BSMR_DIAG")) p.diag = static_cast<u32>(std::atoi(dg));
-    if (const char* po = std::getenv("BSMR_PIECE_ORDER")) p.piece_order = static_cast<u32>(std::atoi(po));
-    if (const char* tm = std::getenv("BSMR_TILE_MIN_F32")) p.tile_min_f32 = static_cast<u32>(std::atoi(tm));
-    if (const char* tm = std::getenv("BSMR_TILE_MIN_HALF")) p.tile_min_half = static_cast<u32>(std::atoi(tm));
-    if (const char* pm = std::getenv("BSMR_PIECE_MAX"))
-        p.piece_max = std::min<u32>(RB_PIECE_MAX, std::max(1, std::atoi(pm)));
-    if (const char* pw = std::getenv("BSMR_PIECE_WEIGHT")) p.piece_weight = std::max(0.0, std::atof(pw));
-    if (const char* sw = std::getenv("BSMR_SHARD_PIECE_WEIGHT"))
-        p.shard_piece_weight = std::max(0.0, std::atof(sw));
-    if (const char* dm = std::getenv("BSMR_DENSE_MIN")) p.dense_min = static_cast<float>(std::atof(dm));
-    if (const char* orr = std::getenv("BSMR_ORIG_ROWS"))  // "0" never, "1" always, else auto
-        p.orig_rows = orr[0] == '0' ? 0 : orr[0] == '1' ? 1 : -1;
-    if (const char* oc = std::getenv("BSMR_ORIG_CONTIG")) p.orig_contig = std::atoi(oc);
-    if (const char* dk = std::getenv("BSMR_DENSE_KS")) p.dense_ks = std::atoi(dk);
-    if (const char* dn = std::getenv("BSMR_DENSE_NS")) p.dense_ns = std::atoi(dn);
-    if (const char* os = std::getenv("BSMR_OUT_STAGED"))  // "0" never, "1" always, else auto
-        p.out_staged = os[0] == '0' ? 0 : os[0] == '1' ? 1 : -1;
-    if (const char* l2 = std::getenv("BSMR_L2_RANGE_KB")) {
-        p.l2_range_kb = std::max(64, std::atoi(l2));
-        p.l2_range_user = true;
+    if (const bsmr_tuning* t = o.tuning) {  // launch-layout knobs; "auto" keeps the defaults
+        p.diag = t->diag;
+        if (t->piece_order >= 0) p.piece_order = static_cast<u32>(t->piece_order);
+        if (t->tile_min_f32 >= 0) p.tile_min_f32 = static_cast<u32>(t->tile_min_f32);
+        if (t->tile_min_half >= 0) p.tile_min_half = static_cast<u32>(t->tile_min_half);
+        if (t->piece_max >= 0) p.piece_max = std::min<u32>(RB_PIECE_MAX, std::max(1, t->piece_max));
+        if (t->piece_weight >= 0) p.piece_weight = t->piece_weight;
+        if (t->shard_piece_weight >= 0) p.shard_piece_weight = t->shard_piece_weight;
+        if (t->dense_min >= 0) p.dense_min = t->dense_min;
+        if (t->orig_rows >= 0) p.orig_rows = t->orig_rows ? 1 : 0;
+        if (t->orig_contig >= 0) p.orig_contig = t->orig_contig;
+        if (t->dense_ks >= 0) p.dense_ks = t->dense_ks;
+        if (t->dense_ns >= 0) p.dense_ns = t->dense_ns;
+        if (t->out_staged >= 0) p.out_staged = t->out_staged ? 1 : 0;
+        if (t->l2_range_kb >= 0) {
+            p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
+            p.l2_range_user = true;
+        }
     }
     return BSMR_OK;
 }
@@ -189,7 +237,24 @@ extern "C" int bsmr_plan_import_rows(const uint32_t* rowptr, const uint32_t* col
     p.nnz = hdr->nnz;
     int st = init_plan(p, o);
     if (st != BSMR_OK) return fail(st);
-    // the rows must be the non-empty rows of S, each once (they index rowptr on the device)
+    // the column-stage geometry must be the one bsmr_plan_create derives from (M, N, bs)
+    // (rowReordering.cu:1035, 911-920); bs itself depends on the exporter's free memory
+    if (hdr->block_size < 16 || hdr->block_size > 65535 ||
+        hdr->num_blocks_per_row !=
+            static_cast<u32>(std::ceil(static_cast<float>(hdr->N) / static_cast<float>(hdr->block_size))) ||
+        hdr->cluster_block_dim != cluster_block_dim(hdr->num_blocks_per_row)) {
+        set_error("bsmr_plan_import_rows: block_size / num_blocks_per_row / cluster_block_dim "
+                  "inconsistent with N");
+        return fail(BSMR_ERR_INVALID);
+    }
+    // the rows must be the non-empty rows of S, each once (they index rowptr on the device):
+    // num_zero_rows equal to S's empty-row count, R distinct non-empty rows, R + z == M
+    u32 empty = 0;
+    for (u32 r = 0; r < M; ++r) empty += rowptr[r] == rowptr[r + 1];
+    if (empty != hdr->num_zero_rows) {
+        set_error("bsmr_plan_import_rows: num_zero_rows differs from the empty rows of S");
+        return fail(BSMR_ERR_INVALID);
+    }
     std::vector<u32> hrows(R);
     if (R && hipMemcpy(hrows.data(), rows, static_cast<size_t>(R) * sizeof(u32), hipMemcpyDefault) !=
                  hipSuccess) {

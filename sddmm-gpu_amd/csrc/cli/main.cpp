@@ -94,14 +94,18 @@ void run_sddmm(bsmr_plan* plan, const bsmr_csr* S, uint32_t K, int iters, cli::L
 // checkSddmm (sddmm.cu:41-59), compiled in by the reference's `#define VALIDATE` (sddmm.cu:7) and
 // switched on here by BSMR_VALIDATE=1 (the flags stay the reference's): host SDDMM of the same
 // operands, checkData's framed report, and the NO PASS line on mismatches.
-// BSMR_VALIDATE_CORRUPT=n (fault injection for tests): add 1 to the first n GPU values first.
+// Fault injection exists only in the test build (bin/BSMR-sddmm-faultinject, -DBSMR_FAULT_INJECT):
+// BSMR_VALIDATE_CORRUPT=n adds 1 to the first n GPU values first. The release binary has no such
+// hook, so no environment variable can alter its reported check.
 bool check_sddmm(const bsmr_csr* S, uint32_t K, const Operands& ops, std::vector<float>& P) {
     uint32_t M, N, nnz;
     bsmr_csr_info(S, &M, &N, &nnz);
+#ifdef BSMR_FAULT_INJECT
     if (const char* c = std::getenv("BSMR_VALIDATE_CORRUPT")) {
         const long n = std::min<long>(std::atol(c), static_cast<long>(P.size()));
         for (long i = 0; i < n; ++i) P[i] += 1.0f;
     }
+#endif
     std::vector<float> Pcpu(nnz);
     int st = bsmr_sddmm_cpu(bsmr_csr_rowptr(S), bsmr_csr_colidx(S), M, N, K, ops.A.data(),
                             ops.B.data(), Pcpu.data(), 0);

@@ -597,28 +597,43 @@ __device__ __forceinline__ void load_bcol(const RbArgs& a, const u32 col, const 
 // in one column. Lane s of the group holds the metadata of entries first + G*k + s.
 template <int RBY>
 struct Piece {
-    u32 first, len;
+    u32 first, len, col;
     u32 mm[RowGeom<RBY>::NB], mo[RowGeom<RBY>::NB];
 };
+
+// the piece descriptor (first entry, column, length)
+template <int RBY>
+__device__ __forceinline__ void load_piece_desc(const RbArgs& a, const u32 pi, Piece<RBY>& pc) {
+    const uint2 d = a.pieces[pi];
+    pc.first = d.x;
+    pc.len = (d.y >> 22) + 1;
+    pc.col = d.y & 0x3FFFFFu;
+}
+
+// the piece's B column and its entries' metadata (after load_piece_desc)
+template <int RBY>
+__device__ __forceinline__ void load_piece_body(const RbArgs& a, const u32 sub,
+                                                const u32 (&rot)[RowGeom<RBY>::NC],
+                                                f32x4 (&bv)[RowGeom<RBY>::NC], Piece<RBY>& pc) {
+    constexpr u32 G = RowGeom<RBY>::G;
+    load_bcol<RBY>(a, pc.col, sub, rot, bv);
+#pragma unroll
+    for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
+        const u32 e = G * k + sub;
+        pc.mm[k] = e < pc.len ? a.meta[pc.first + e] : 0u;
+        // staged output: the slot is the metadata's low bits, taken where the result is stored
+        // (deriving it here made the prologue wait for this load, and so for the B column
+        // before it, ahead of the staging)
+        pc.mo[k] = !a.outLds && e < pc.len ? a.out[pc.first + e] : 0u;
+    }
+}
 
 template <int RBY>
 __device__ __forceinline__ void load_piece(const RbArgs& a, const u32 pi, const u32 sub,
                                            const u32 (&rot)[RowGeom<RBY>::NC],
                                            f32x4 (&bv)[RowGeom<RBY>::NC], Piece<RBY>& pc) {
-    constexpr u32 G = RowGeom<RBY>::G;
-    const uint2 d = a.pieces[pi];
-    pc.first = d.x;
-    pc.len = (d.y >> 22) + 1;
-    load_bcol<RBY>(a, d.y & 0x3FFFFFu, sub, rot, bv);
-#pragma unroll
-    for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
-        const u32 e = G * k + sub;
-        pc.mm[k] = e < pc.len ? a.meta[pc.first + e] : 0u;
-        if (a.outLds)
-            pc.mo[k] = pc.mm[k] & 0x3FFFFFu;  // the slot
-        else
-            pc.mo[k] = e < pc.len ? a.out[pc.first + e] : 0u;
-    }
+    load_piece_desc<RBY>(a, pi, pc);
+    load_piece_body<RBY>(a, sub, rot, bv, pc);
 }
 
 // Step i of a batch of G computes entry G*k + i in all G lanes; lane i keeps it, so a batch ends
@@ -684,8 +699,9 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
             if (sub == static_cast<u32>(i)) res = sm;
         }
         if (sub < nb) {
-            if (a.outLds)
-                *reinterpret_cast<float*>(const_cast<char*>(As) + a.outLds + 4 * pc.mo[k]) = res;
+            if (a.outLds)  // the slot: rank by CSR position inside the item
+                *reinterpret_cast<float*>(const_cast<char*>(As) + a.outLds +
+                                          4 * (pc.mm[k] & 0x3FFFFFu)) = res;
             else
                 a.P[pc.mo[k]] = res;
         }
@@ -707,7 +723,13 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     constexpr u32 NG = NT / G;                // residual row-groups
     constexpr u32 TC = DenseTileLds<DT, RBY>::CH;
     const unsigned long long t0 = rtime(a.trace);
-    const uint4 it = a.items[blockIdx.x];
+    uint4 it = a.items[blockIdx.x];
+    // all four fields in SGPRs before the padding test: the compiler otherwise loads .x (the row
+    // block) in a second, dependent round trip after the test
+    it.x = __builtin_amdgcn_readfirstlane(it.x);
+    it.y = __builtin_amdgcn_readfirstlane(it.y);
+    it.z = __builtin_amdgcn_readfirstlane(it.z);
+    it.w = __builtin_amdgcn_readfirstlane(it.w);
     const u32 pend = a.itemEnd[blockIdx.x];
     if (it.y == it.z && it.w == pend) return;  // padding item (uniform across the workgroup)
     const u32 q0 = a.qbase + it.x * a.RB;
@@ -721,14 +743,6 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
 #pragma unroll
     for (u32 f = 0; f < NC; ++f) rot[f] = 16u * G * ((f + j % Geo::RR) % NC);
-    f32x4 tb[TC], pre[NC];
-    DenseTileLds<DT, RBY> dt;
-    // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
-    const u32 tw = NW - 1 - w;
-    if (tw < ntile) dt.load(a, a.tileIds[it.y + tw], q0, tb);
-    Piece<RBY> pc;
-    pc.len = 0;
-    if (gr < np) load_piece<RBY>(a, it.w + gr, sub, rot, pre, pc);
     // stage the row block by LDS-DMA: each wave-instruction fills one contiguous KiB of the image
     // (64 chunks of the row-major image); lane l supplies image chunk x = 64 b + l, i.e. row
     // lr = x / NCH at physical chunk pc = x % NCH, read from the logical chunk lds_chunk(lr, pc)
@@ -740,23 +754,46 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // LDS-DMAs (a ds_bpermute hand-out of the row indices did this), makes the compiler wait
     // (vmcnt(0)) for each LDS-DMA before issuing the next, which serialised the staging
     // (C2: 12.8 -> 12.0 us once removed).
+    constexpr u32 NCH = RBY / 16;
+    constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
+    constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
+    static_assert(MAXB * NW == (NT == 1024 ? 160u : 80u), "whole KiB blocks");
+    constexpr bool ROWV = MAXB * NR <= 64;  // one row index per lane (else 128-byte rows)
+    const u32 lane = tid & 63;
+    const u32 ws = __builtin_amdgcn_readfirstlane(w);  // wave index in an SGPR
+    // the staging row indices are loaded first: they depend only on the item, so their round
+    // trip overlaps the piece descriptor's, and the LDS-DMAs need not wait for the B columns
+    u32 rowv = a.row0;
+    u32 src[ROWV ? 1 : MAXB];
+    if constexpr (ROWV) {
+        const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
+        if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
+    } else {
+        // 128-byte rows: 8 rows per block, too many indices for one per lane; each lane loads
+        // the row of its own chunk for every block
+#pragma unroll
+        for (u32 i = 0; i < MAXB; ++i) {
+            const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
+            src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
+        }
+    }
+    // the loads the LDS-DMA issue waits for go first: row indices, the phase-0 piece descriptor
+    // and the first tile's metadata (one round trip together); the B columns and entry metadata
+    // they address are issued after the LDS-DMAs, so the staging never waits for a B gather
+    f32x4 tb[TC], pre[NC];
+    DenseTileLds<DT, RBY> dt;
+    // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
+    const u32 tw = NW - 1 - w;
+    Piece<RBY> pc;
+    pc.len = 0;
+    if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
+    if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
     {
-        constexpr u32 NCH = RBY / 16;
-        constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
-        constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
-        static_assert(MAXB * NW == (NT == 1024 ? 160u : 80u), "whole KiB blocks");
-        const u32 lane = tid & 63;
-        const u32 ws = __builtin_amdgcn_readfirstlane(w);  // wave index in an SGPR
         // the source chunk of lane l is the same in every block of the wave: x % NCH and
         // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
         const u32 x0 = 64 * ws + lane;
         const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
-        if constexpr (MAXB * NR <= 64) {
-            u32 rowv = a.row0;
-            {
-                const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
-                if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
-            }
+        if constexpr (ROWV) {
 #pragma unroll
             for (u32 i = 0; i < MAXB; ++i) {
                 const u32 b = ws + i * NW;
@@ -772,14 +809,6 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                                                  16, 0, 0);
             }
         } else {
-            // 128-byte rows: 8 rows per block, too many indices for one per lane; each lane loads
-            // the row of its own chunk for every block (all loads first, then the LDS-DMAs)
-            u32 src[MAXB];
-#pragma unroll
-            for (u32 i = 0; i < MAXB; ++i) {
-                const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
-                src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
-            }
 #pragma unroll
             for (u32 i = 0; i < MAXB; ++i) {
                 const u32 b = ws + i * NW;
@@ -790,6 +819,12 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             }
         }
     }
+    if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
+    if (tw < ntile) dt.loadB(a, 0, tb);
+    // every LDS-DMA of the workgroup has landed before any wave reads the image or writes the
+    // staged-output slots (the blocks past the image land in the tail those slots use); explicit,
+    // not left to the compiler's wait insertion at the barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const unsigned long long tm = rtime(a.trace);
     if (a.diag & 8) {  // staging only

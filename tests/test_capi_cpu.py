@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in sorted(declared) if not hasattr(L, s)]
     assert not missing, missing
     assert declared == set(bsmr.EXPORTS), declared ^ set(bsmr.EXPORTS)
-    assert L.bsmr_abi_version() == bsmr.ABI_VERSION == 5
+    assert L.bsmr_abi_version() == bsmr.ABI_VERSION == 6
 
 
 def test_rocsparse_baseline_exports_every_header_symbol():
@@ -128,3 +128,24 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(bsmr, "LIB_PATH", "/nonexistent/libbsmr_amd.so")
     with pytest.raises(bsmr.BsmrError):
         bsmr.lib()
+
+
+def test_tuning_env_parser_matches_python_mapping(monkeypatch):
+    """bsmr_tuning_from_env (the library's parser, called explicitly by tools) and the Python
+    mapping the tests use give the same knobs; nothing is read unless asked."""
+    import bsmr
+    env = {"BSMR_TILE_MIN_F32": "0", "BSMR_OUT_STAGED": "1", "BSMR_ORIG_ROWS": "auto",
+           "BSMR_PIECE_WEIGHT": "2.5", "BSMR_L2_RANGE_KB": "64", "BSMR_DIAG": "8"}
+    for k in bsmr.TUNING_ENV.values():
+        monkeypatch.delenv(k, raising=False)
+    assert bsmr.tuning_from_env() == {}
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from_c = bsmr.tuning_from_env()
+    from_py = bsmr.tuning_from_env(env)
+    assert from_py == {"tile_min_f32": 0, "out_staged": 1, "orig_rows": -1,
+                       "piece_weight": 2.5, "l2_range_kb": 64, "diag": 8}
+    # orig_rows "auto" equals the default (-1), so the C parser reports no change for it
+    assert from_c == {k: v for k, v in from_py.items() if k != "orig_rows"}
+    with pytest.raises(bsmr.BsmrError):
+        bsmr._tuning_struct({"no_such_knob": 1})

@@ -93,6 +93,17 @@ def _worker(rank, world, port, q):
     if rank == 0:
         res["p2_errors"] = O.check_data(ref, Pg2)
         res["p2_written"] = int(np.count_nonzero(Pg2))
+    # the same segments gathered as they are (bench.py's local split): bit-exact, including the
+    # sign of a zero output, which the sum-reduce loses (-0.0 + 0.0 = +0.0)
+    e0, e1 = int(rp[q0]), int(rp[q1])
+    seg = P2[e0:e1].copy()
+    seg[0] = -0.0
+    Pg3 = D.gather_segments(torch.from_numpy(seg), e0, e1, len(ci), 0)
+    Pall = D.gather_segments(torch.from_numpy(P2[e0:e1].copy()), e0, e1, len(ci), 0)
+    if rank == 0:
+        res["seg_equal"] = bool(np.array_equal(Pall.view(np.uint32), Pg2.view(np.uint32)))
+        res["seg_negzero"] = [bool(np.signbit(Pg3[int(rp[q])]) and Pg3[int(rp[q])] == 0)
+                              for q in (0, 300)]
     import torch.distributed as dist
     dist.destroy_process_group()
     q.put(res)
@@ -120,6 +131,7 @@ def test_gloo_world2_row_stage_shards_and_p_gather():
     assert r0["p_errors"] == 0 and r0["p_written"] == r0["nnz"]
     assert r0["local_cut"] == (0, 300) and r1["local_cut"] == (300, 600)  # the two copies
     assert r0["p2_errors"] == 0 and r0["p2_written"] == r0["nnz"]
+    assert r0["seg_equal"] and r0["seg_negzero"] == [True, True]
 
 
 def test_row_range_cut():

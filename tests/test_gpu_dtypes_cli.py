@@ -7,13 +7,15 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from bsmr import BF16, F16, Plan, make_data, synth
+from bsmr import BF16, F16, Plan, make_data, synth, tuning_from_env
 from gpu_util import torch_cuda
 
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "sddmm-gpu_amd", "bin", "BSMR-sddmm")
+# the same CLI built with -DBSMR_FAULT_INJECT (honours BSMR_VALIDATE_CORRUPT); test use only
+BIN_FI = os.path.join(ROOT, "sddmm-gpu_amd", "bin", "BSMR-sddmm-faultinject")
 FREE = 288 * 1024 ** 3
 
 
@@ -74,19 +76,18 @@ def test_half_inputs_checkdata(dtype, K, case, layout):
     ("zipf", 128, BF16, True),          # sparse pattern forced dense: empty tiles skipped
     ("zipf", 256, F16, True),
 ])
-def test_dense_sampled_half(monkeypatch, case, K, dtype, force):
+def test_dense_sampled_half(case, K, dtype, force):
     """The dense-sampled MFMA launch (whole 128 x 128 tiles of A B^T, sampled) for fp16/bf16
     patterns above the density threshold (layout auto), against the oracle on the rounded
     values."""
-    if force:
-        monkeypatch.setenv("BSMR_DENSE_MIN", "0")
+    tun = tuning_from_env({"BSMR_DENSE_MIN": "0"} if force else {})
     if case == "uniform300":
         M, N, rp, ci = synth.uniform_mask(300, 0.2, seed=5)
     elif case == "zipf":
         M, N, rp, ci = synth.random_rows(400, 3000, 50, seed=8, zipf=1.1)
     else:
         M, N, rp, ci = synth.block_mask(512, 16, 0.1, seed=7)
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, tuning=tun)
     conv = to_bf16_bits if dtype == BF16 else to_f16_bits
     Ab, Ar = conv(make_data(M * K))
     Bb, Br = conv(make_data(N * K)[::-1].copy())
@@ -104,13 +105,12 @@ def test_dense_sampled_half(monkeypatch, case, K, dtype, force):
     ({"BSMR_DENSE_NS": "5"}, 128, BF16),   # fewer chunks than stages
     ({"BSMR_DENSE_NS": "5"}, 512, F16),
 ])
-def test_dense_sampled_variants(monkeypatch, env, K, dtype):
+def test_dense_sampled_variants(env, K, dtype):
     """Every wave/stage form of the dense-sampled launch (sddmm_dense.hip launch_dense) gives the
     oracle's values on a ragged 300 x 300 pattern (edge tiles read clamped rows)."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     M, N, rp, ci = synth.uniform_mask(300, 0.2, seed=11)
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,
+                tuning=tuning_from_env(env))
     conv = to_bf16_bits if dtype == BF16 else to_f16_bits
     Ab, Ar = conv(make_data(M * K))
     Bb, Br = conv(make_data(N * K)[::-1].copy())
@@ -246,15 +246,20 @@ def _oracle_report(n, n_err_vals=None):
 def test_cli_validate_checkdata_surface(tmp_path, corrupt):
     """BSMR_VALIDATE=1 (the reference's VALIDATE build, sddmm.cu:34-59): the host SDDMM of the same
     operands, checkData's framed block before the log, and on a deliberately corrupted P
-    (BSMR_VALIDATE_CORRUPT=n adds 1 to the first n GPU values) the errors and the NO PASS line."""
+    (BSMR_VALIDATE_CORRUPT=n adds 1 to the first n GPU values; only the test build BIN_FI has that
+    hook, the release binary ignores the variable) the errors and the NO PASS line."""
     M, N, rp, ci = synth.random_rows(500, 1500, 30, seed=13, zipf=1.05)
     path = str(tmp_path / "v.mtx")
     synth.write_mtx(path, M, N, rp, ci)
     env = dict(os.environ, BSMR_VALIDATE="1")
     if corrupt:
         env["BSMR_VALIDATE_CORRUPT"] = str(corrupt)
-    r = subprocess.run([BIN, "-f", path, "-k", "64"], capture_output=True, text=True,
-                       timeout=300, env=env)
+        # the release binary has no fault-injection hook: the variable changes nothing
+        r = subprocess.run([BIN, "-f", path, "-k", "64"], capture_output=True, text=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0 and "NO PASS" not in r.stdout, r.stderr
+    r = subprocess.run([BIN_FI if corrupt else BIN, "-f", path, "-k", "64"], capture_output=True,
+                       text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     out = r.stdout
     head = "check cpu sddmm and BSMR sddmm: \n"

@@ -5,8 +5,10 @@ HIP SDDMM against the oracle's host SDDMM (host.cpp:45-76 loop order) by the che
 * C2 nips-like, fp32, K = 128 (the bench line's workload);
 * C3 cop20k_A-like 121,192^2, fp16 A/B (the oracle runs in fp32 on the same rounded values:
   half x half products are exact in fp32), K = 256;
-* C4 reddit-like at scale 0.5 (116,482^2, 58 M stored entries), fp32, K = 128, whole-plan launch
-  and a 4-way row-panel split with shard-local A rows;
+* C4 reddit-like at its BASELINE size (232,965^2, 232 M stored entries), fp32, K = 128, in the
+  three forms bench.py runs: the whole-plan launch, the 8-way row-panel split of the one global
+  plan (bsmr_sddmm_panels_local, shard-local A rows) and the 8 local per-panel plans (contiguous
+  original row panels of equal stored entries, each with its own plan);
 * C5 DLMC-like 2048^2 90 %-sparse masks (uniform: the dense-sampled MFMA launch; 16x16 blocks: the
   column-major tile launch), bf16, K = 512.
 """
@@ -30,7 +32,7 @@ def _pattern(name):
     if name == "C3":
         return synth.cop20k_like()
     if name == "C4":
-        return synth.reddit_like(0.5)
+        return synth.reddit_like(1.0)
     return synth.dlmc_like(name[3:])
 
 
@@ -67,9 +69,31 @@ def test_full_workload_every_entry(name, K, dtype):
     P = _gpu(plan, A, B, K, len(ci), dtype)
     assert np.isfinite(P).all()
     assert O.check_data(ref, P) == 0
-    if name == "C4":  # the north_star split: 4 row-panel shards, each with only its A rows
+    del P
+    if name == "C4":  # the north_star split: 8 row-panel shards, each with only its A rows
         rows = plan.array("reorderedRows")
-        shards = [plan.shard(K, r, 4, dtype) for r in range(4)]
+        shards = [plan.shard(K, r, 8, dtype) for r in range(8)]
+        assert shards[0][0] == 0 and shards[-1][1] == plan.stats()["num_row_panels"]
+        assert all(a[1] == b[0] for a, b in zip(shards, shards[1:]))
         Ps = _gpu(plan, A, B, K, len(ci), dtype, shards=shards, rows=rows)
         assert np.isfinite(Ps).all()
         assert O.check_data(ref, Ps) == 0
+        del Ps, plan
+        # the local split: 8 contiguous original row panels, each planned on its own
+        torch = torch_cuda()
+        dB = torch.from_numpy(B).cuda()
+        dP = torch.full((len(ci),), float("nan"), dtype=torch.float32, device="cuda")
+        rp64 = np.asarray(rp, dtype=np.int64)
+        for r in range(8):
+            r0, r1 = D.row_range_cut(rp64, r, 8)
+            e0, e1 = int(rp64[r0]), int(rp64[r1])
+            lp = Plan(r1 - r0, N, (rp64[r0:r1 + 1] - e0).astype(np.uint32), ci[e0:e1],
+                      alpha=0.3, delta=0.3)
+            dA = torch.from_numpy(np.ascontiguousarray(A[r0 * K:r1 * K])).cuda()
+            lp.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP[e0:e1].data_ptr(),
+                     stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            del lp, dA
+        Pl = dP.cpu().numpy()
+        assert np.isfinite(Pl).all()
+        assert O.check_data(ref, Pl) == 0

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from bsmr import Plan, make_data, synth
+from bsmr import Plan, make_data, synth, tuning_from_env
 from golden_common import (ALPHAS, DELTAS, REF_FREE_MEM, compare, expected_from_stats, matrix,
                            record)
 from gpu_util import assert_plans_equal, half_values, oracle_plan, run_sddmm, torch_cuda
@@ -243,14 +243,14 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     ({"BSMR_OUT_STAGED": "1", "BSMR_ORIG_ROWS": "1"}, 128, 0),
     ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "64", "BSMR_TILE_MIN_F32": "0"}, 64, 0),
 ])
-def test_rowblock_layout_variants(monkeypatch, env, K, dtype):
+def test_rowblock_layout_variants(env, K, dtype):
     """Launch-layout switches (tile demotion thresholds, L2 column ranges, piece order) on the
     blocky pattern (dense tiles and residual entries) and a zipf pattern: values unchanged."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    tun = tuning_from_env(env)  # the knobs by their BSMR_* names (bsmr_tuning_from_env)
     for name in ("blocky", "wide_bs20"):
         M, N, rp, ci = small_cases()[name]
-        plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock")
+        plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock",
+                    tuning=tun)
         A = make_data(M * K)
         B = make_data(N * K)
         P = run_sddmm(plan, A, B, K, len(ci), dtype=dtype)

@@ -77,6 +77,20 @@ def test_import_rows_rejects_bad_rows():
     bad[0] = M  # out of range
     with pytest.raises(Exception):
         Plan.from_row_stage(rp, ci, hdr, bad)
+    # an inflated zero-row count with one non-empty row dropped: R + z == M still holds and the
+    # rows are distinct and non-empty, but a row of S would never be computed
+    h2 = RowStage.from_array(hdr.to_array())
+    h2.num_zero_rows += 1
+    h2.num_reordered_rows -= 1
+    with pytest.raises(Exception, match="num_zero_rows"):
+        Plan.from_row_stage(rp, ci, h2, rows[1:].copy())
+    # column-stage geometry not derived from N
+    for field, v in (("block_size", 0), ("num_blocks_per_row", hdr.num_blocks_per_row + 1),
+                     ("cluster_block_dim", hdr.cluster_block_dim + 32)):
+        h3 = RowStage.from_array(hdr.to_array())
+        setattr(h3, field, v)
+        with pytest.raises(Exception, match="inconsistent"):
+            Plan.from_row_stage(rp, ci, h3, rows)
 
 
 def _run_local(plan, rows, A, B, K, nnz, shards, dtype):
@@ -104,16 +118,16 @@ def _run_local(plan, rows, A, B, K, nnz, shards, dtype):
     ("zipf", 512, 0, 5),
 ])
 @pytest.mark.parametrize("staged", ["0", "1"])
-def test_panels_local_every_output_once(monkeypatch, name, K, dtype, world, staged):
+def test_panels_local_every_output_once(name, K, dtype, world, staged):
     """Each shard writes exactly its panels' entries from its own A rows (NaN elsewhere stays
     NaN); together they equal the oracle. world 1 on the banded case: the whole range, whose
     plan-wide layout uses original-order row blocks, runs the reordered layout instead. staged:
     results through LDS in CSR order (BSMR_OUT_STAGED) or one store per entry."""
-    monkeypatch.setenv("BSMR_OUT_STAGED", staged)
     M, N, rp, ci = _cases()[name]
     # (the blocky mask is tile-dominated: its auto launch is column-major, so force row blocks)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,
-                layout="rowblock" if name == "blocky" else "auto")
+                layout="rowblock" if name == "blocky" else "auto",
+                tuning={"out_staged": int(staged)})
     rows = plan.array("reorderedRows")
     shards = [plan.shard(K, r, world, dtype) for r in range(world)]
     A = make_data(M * K)
@@ -140,7 +154,9 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("extra", [["--config", "C2"], ["--config", "C2", "--shard", "global"],
+@pytest.mark.parametrize("extra", [["--config", "C2", "--strong", "off"],
+                                   ["--config", "C2", "--shard", "global", "--strong", "off"],
+                                   ["--config", "C2", "--strong-scale", "0.05"],
                                    ["--config", "C4", "--scale", "0.05"],
                                    ["--config", "C4", "--scale", "0.05", "--shard", "global"]])
 def test_bench_sharded_two_ranks_one_gpu(extra):
@@ -167,3 +183,39 @@ def test_bench_sharded_two_ranks_one_gpu(extra):
         assert sum(sh["panels"]) == out["config"]["num_row_panels"]
         assert min(sh["panels"]) > 0
     assert out["scaling"] == ("weak" if "C2" in extra else "strong")
+    if "--strong-scale" in extra:  # the default N > 1 line carries the north_star reddit split
+        sc = out["strong_C4"]
+        for split in ("global", "local"):
+            assert "error" not in sc[split], sc[split]
+            assert sc[split]["checkData_errors_gathered_P"] == 0, split
+            assert len(sc[split]["shards"]["ms_per_step"]) == 2
+    else:
+        assert "strong_C4" not in out
+
+
+@pytest.mark.timeout(600)
+def test_bench_sharded_rccl_one_rank():
+    """bench.py's multi-GPU path on RCCL (backend "nccl"), launched by torchrun before any GPU
+    call, at world size 1 (--force-sharded: RCCL refuses two ranks on one device): RCCL init, the
+    device-tensor broadcasts (B, row stage, the strong_C4 pattern), the P sum-reduce and the
+    segment gather all execute on MI355X; both strong_C4 splits and the C2 line pass checkData."""
+    env = dict(os.environ, OMP_NUM_THREADS="8")
+    env.pop("BSMR_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--force-sharded", "--steps", "5",
+           "--warmup", "2", "--strong", "on", "--strong-scale", "0.1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=540, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    out = json.loads(line[0])
+    assert out["config"]["backend"] == "nccl"
+    assert out["n_gpus"] == 1 and out["checkData_errors_gathered_P"] == 0
+    sc = out["strong_C4"]
+    for split in ("global", "local"):
+        assert "error" not in sc[split], sc[split]
+        assert sc[split]["checkData_errors_gathered_P"] == 0, split
+        assert sc[split]["ms_per_step"] > 0
+    assert sc["global"]["whole_plan_one_gpu"]["ms_per_step"] > 0
+    assert sum(sc["global"]["shards"]["entries"]) == sc["nnz"]

@@ -25,7 +25,7 @@ def main():
     import torch
 
     import bsmr
-    from bsmr import Plan, make_data, synth
+    from bsmr import Plan, make_data, synth, tuning_from_env
 
     code = bsmr.BF16 if args.dtype == "bf16" else bsmr.F16
     tdt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
@@ -40,7 +40,7 @@ def main():
         res = {}
         for name, env in (("dense", "0"), ("gather", "2")):
             os.environ["BSMR_DENSE_MIN"] = env  # read at plan creation
-            plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3)
+            plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, tuning=tuning_from_env())
             dP = torch.zeros(len(ci), dtype=torch.float32, device="cuda")
             call = lambda: plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),  # noqa: E731
                                       stream=s.cuda_stream, dtype=code)

@@ -32,7 +32,7 @@ def main():
     import torch
 
     import bsmr
-    from bsmr import Plan, make_data, synth
+    from bsmr import Plan, make_data, set_default_tuning, synth, tuning_from_env
 
     gen = getattr(synth, args.workload)
     if args.mask is not None:
@@ -40,6 +40,7 @@ def main():
     else:
         M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
     K = args.K
+    set_default_tuning(tuning_from_env())  # BSMR_* A/B knobs (the library reads no env)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout,
                 lds_budget_kb=args.lds_kb)
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]

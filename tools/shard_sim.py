@@ -41,7 +41,7 @@ def main():
 
     import bsmr
     import oracle_lib as O
-    from bsmr import Plan, make_data, synth
+    from bsmr import Plan, make_data, set_default_tuning, synth, tuning_from_env
 
     gen = getattr(synth, args.workload)
     M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
@@ -52,6 +52,7 @@ def main():
     code = {"f32": bsmr.F32, "f16": bsmr.F16, "bf16": bsmr.BF16}[args.dtype]
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
     t0 = time.perf_counter()
+    set_default_tuning(tuning_from_env())  # BSMR_* A/B knobs (the library reads no env)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3)
     plan_s = time.perf_counter() - t0
     print(f"plan {plan_s:.1f} s", file=sys.stderr, flush=True)

@@ -80,6 +80,54 @@ def k512(name, M, N, rp, ci, iters=10):
             "ms": round(best[3], 5), "grid": grid}
 
 
+def retime_and_cpu(M, N, rp, ci, K, alpha, delta, iters=100):
+    """The best setting re-timed through the C ABI (HIP events over `iters` back-to-back launches,
+    the log prints bsmr_sddmm with 2 decimals only), its HBM roofline fraction (algorithmic bytes
+    4K(M+N) + 8 nnz + 4(M+1), SURVEY.md §8d, against 8 TB/s) and the same-box CPU rate: the
+    product's OpenMP host SDDMM (host.cpp:45-76 restated) on all host cores, median of 3 after a
+    warm-up, with checkData of the GPU P against it."""
+    import statistics
+
+    import torch
+
+    from bsmr import Plan, check_data, make_data, sddmm_cpu
+
+    A = make_data(M * K)
+    B = make_data(N * K)
+    dA = torch.from_numpy(A).cuda()
+    dB = torch.from_numpy(B).cuda()
+    dP = torch.zeros(len(ci), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    plan = Plan(M, N, rp, ci, alpha=alpha, delta=delta)
+    for _ in range(3):
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s.cuda_stream)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s.cuda_stream)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    nnz = len(ci)
+    flops = 2.0 * nnz * K
+    bytes_alg = 4.0 * K * (M + N) + 8.0 * nnz + 4.0 * (M + 1)
+    threads = os.cpu_count() or 1
+    sddmm_cpu(M, N, rp, ci, K, A, B, threads=threads)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        P = sddmm_cpu(M, N, rp, ci, K, A, B, threads=threads)
+        ts.append(time.perf_counter() - t0)
+    cpu_s = statistics.median(ts)
+    return {"event_ms": round(ms, 5), "event_gflops": round(flops / (ms * 1e-3) / 1e9, 2),
+            "roofline_frac": round(bytes_alg / (ms * 1e-3) / 8e12, 4),
+            "bytes_alg": bytes_alg,
+            "cpu_gflops": round(flops / cpu_s / 1e9, 2), "cpu_ms": round(cpu_s * 1e3, 3),
+            "cpu_threads": threads,
+            "checkData_errors_gpu_vs_cpu": check_data(P, dP.cpu().numpy())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/ss")
@@ -93,7 +141,14 @@ def main():
     os.makedirs(args.out, exist_ok=True)
     pub = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_published_gflops.json")))
     published = {(r["matrix"], r["K"]): r for r in pub["rows"]}
+    cpu = ""
+    try:
+        cpu = [x.split(":", 1)[1].strip() for x in open("/proc/cpuinfo")
+               if x.startswith("model name")][0]
+    except (OSError, IndexError):
+        pass
     result = {"hardware": "AMD Instinct MI355X (1 GPU)", "reference_hardware": pub["hardware"],
+              "cpu": cpu,
               "rule": "best bsmr_gflops over alpha x delta (analyze_results.cpp:283-345), "
                       "10 back-to-back launches per setting (warm, as the reference)",
               "matrices": {}}
@@ -132,6 +187,8 @@ def main():
                  "test_mode_s": round(t2 - t1, 1), "K": per_k}
         if not args.no_k512:
             entry["K"]["512"] = k512(name, M, N, rp, ci)
+        for K, v in entry["K"].items():
+            v.update(retime_and_cpu(M, N, rp, ci, int(K), v["alpha"], v["delta"]))
         result["matrices"][name] = entry
         print(json.dumps({name: {k: (v["mi355x_gflops"] if "mi355x_gflops" in v else v["gflops"])
                                  for k, v in entry["K"].items()}}), flush=True)
