@@ -158,7 +158,8 @@ void fill_plan_fields(bsmr_plan* plan, uint32_t K, cli::Logger& log) {
 
 void base_fields(const cli::Options& o, const bsmr_csr* S, uint32_t K, cli::Logger& log) {
     hipDeviceProp_t prop{};
-    if (hipGetDeviceProperties(&prop, 0) == hipSuccess) log.gpu = prop.name;
+    if (hipGetDeviceProperties(&prop, 0) == hipSuccess)  // (cudaDeviceProp::name, Logger.hpp:23-25)
+        log.gpu = prop.name[0] ? prop.name : prop.gcnArchName;  // MI355X reports no marketing name
     log.inputFile = o.inputFile();
     uint32_t M, N, nnz;
     bsmr_csr_info(S, &M, &N, &nnz);
