@@ -80,6 +80,9 @@ def parse():
     ap.add_argument("--strong", default="auto", choices=["auto", "on", "off"],
                     help="strong_C4 block (the north_star reddit row-panel split, both splits, "
                          "with the global plan's N = 1 point); auto = for C2 at N > 1")
+    ap.add_argument("--rebalance", type=int, default=2,
+                    help="global split: rounds of measured-cost re-cutting "
+                         "(bsmr_plan_shard_rebalance) before the timed steps")
     ap.add_argument("--strong-scale", type=float, default=1.0,
                     help="reddit-like size of the strong_C4 block (1 = 232 M stored entries)")
     ap.add_argument("--cold-steps", type=int, default=20,
@@ -205,7 +208,7 @@ def vendor_baseline(M, N, K, rp, ci, dA, dB, P_engine, dtype, stream, flops, eng
         try:
             call()
         except BsmrError as e:
-            out[alg] = {"error": str(e)[-160:]}
+            out[alg] = {"error": str(e)[-400:]}
             continue
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -691,7 +694,7 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
     import numpy as np
     import torch
 
-    from bsmr import make_data
+    from bsmr import BsmrError, make_data
     from bsmr import dist as D
 
     (M, N, rp, ci), K, dtype, desc, scaling = wl
@@ -700,7 +703,9 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
                                     layout=args.layout)
     st = plan.stats()
     t0 = time.perf_counter()
-    p0, p1 = plan.shard(K, rank, world, dtype)  # same cuts on every rank (same global plan)
+    # the same cuts on every rank (same global plan): the model's, then re-balanced by measured
+    # shard times (bsmr_plan_shard_rebalance) for args.rebalance rounds
+    cuts = [plan.shard(K, r, world, dtype)[0] for r in range(world)] + [st["num_row_panels"]]
     cut_s = time.perf_counter() - t0
     rows = plan.array("reorderedRows")
     tdt = {0: torch.float32, 1: torch.float16, 2: torch.bfloat16}[dtype]
@@ -727,17 +732,42 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
         if rank == 0:
             del dA_all, dP1
             torch.cuda.empty_cache()
-    A_local = D.shard_a_rows(A, K, rows, p0, p1)
-    dA = torch.from_numpy(A_local.reshape(-1)).to(dev).to(tdt)
-    if dA.numel() == 0:
-        dA = torch.zeros(K, dtype=tdt, device=dev)
     dP = torch.zeros(nnz, dtype=torch.float32, device=dev)
+    cur = {}
+
+    def use(c):  # this rank's panels of cuts c and their A rows on the device
+        cur["p0"], cur["p1"] = c[rank], c[rank + 1]
+        A_local = D.shard_a_rows(A, K, rows, cur["p0"], cur["p1"])
+        cur["dA"] = torch.from_numpy(A_local.reshape(-1)).to(dev).to(tdt)
+        if cur["dA"].numel() == 0:
+            cur["dA"] = torch.zeros(K, dtype=tdt, device=dev)
 
     def step():
-        if p1 > p0:
-            plan.sddmm_panels_local(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), p0, p1,
-                                    stream=sp, dtype=dtype)
+        if cur["p1"] > cur["p0"]:
+            plan.sddmm_panels_local(cur["dA"].data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+                                    cur["p0"], cur["p1"], stream=sp, dtype=dtype)
 
+    rounds = []
+    best = None
+    for it in range(args.rebalance + 1):
+        use(cuts)
+        ms_r = D.all_values(_timed_steps(step, min(args.steps, 50), args.warmup, stream), dev)
+        rounds.append({"cuts": [int(c) for c in cuts], "ms_per_step": [round(x, 5) for x in ms_r],
+                       "imbalance_max_over_mean": round(max(ms_r) / (sum(ms_r) / world), 3)})
+        if best is None or max(ms_r) < best[0]:
+            best = (max(ms_r), list(cuts))
+        if it == args.rebalance or world == 1:
+            break
+        try:
+            nxt = plan.shard_rebalance(K, world, cuts, ms_r, dtype)
+        except BsmrError:  # not a row-block launch: the per-panel model's cuts stay
+            break
+        if nxt == cuts:
+            break
+        cuts = nxt
+    cuts = best[1]  # the fastest cut seen
+    use(cuts)
+    p0, p1 = cur["p0"], cur["p1"]
     ms_mine = _timed_steps(step, args.steps, args.warmup, stream)
     ms_all = D.all_values(ms_mine, dev)
     lens = np.diff(np.asarray(rp, dtype=np.int64))
@@ -767,6 +797,7 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
         "row_stage_bcast_ms": round(pinfo["row_stage_bcast_ms"], 3),
         "row_stage_bytes": pinfo["row_stage_bytes"],
         "shard_cut_s": round(cut_s, 3),
+        "rebalance_rounds": rounds,
         "b_broadcast_ms": round(bcast_ms, 3),
         "p_gather_ms": round(gather_ms, 3),
         "shards": {

@@ -103,6 +103,8 @@ typedef struct {
                                   1 always, -1 auto (P > 8 MiB) */
     int32_t l2_range_kb;       /* BSMR_L2_RANGE_KB: B bytes per XCD column range (>= 64);
                                   -1 = auto */
+    int32_t stage_nt;          /* BSMR_STAGE_NT: row-block A staging with the nt cache policy, 0
+                                  never, 1 always, -1 auto */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -256,6 +258,14 @@ int bsmr_plan_shard(const bsmr_plan* plan, uint32_t K, int rank, int world, uint
                     uint32_t* p1);
 int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtype, int rank, int world,
                           uint32_t* p0, uint32_t* p1);
+/* Measured-cost rebalancing of the row-block cut: prev_cuts[world+1] are the panel cuts the ranks
+ * ran (bsmr_plan_shard_dtype's, or an earlier rebalance) and shard_ms[world] the time each shard
+ * took; every row block's model cost is scaled by its shard's measured / predicted ratio and the
+ * plan is cut again (cuts[world+1], row-block boundaries). Deterministic in its inputs, so every
+ * rank derives the same cuts from the same gathered times. Row-block launches of reordered
+ * plans only, else BSMR_ERR_UNSUPPORTED. */
+int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int dtype, int world,
+                              const uint32_t* prev_cuts, const float* shard_ms, uint32_t* cuts);
 /* Per-panel cost model on host offset arrays (no device): cuts[world+1], cuts[0]=0,
  * cuts[world]=P. */
 int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* sparseValueOffsets, uint32_t P,

@@ -38,8 +38,10 @@ struct bsmr_rocsparse {
     do {                                                                                 \
         rocsparse_status s_ = (call);                                                    \
         if (s_ != rocsparse_status_success) {                                            \
-            char m_[160];                                                                \
-            std::snprintf(m_, sizeof m_, "%s failed: rocsparse_status %d", #call, (int)s_); \
+            char m_[320];                                                                \
+            std::snprintf(m_, sizeof m_, "rocsparse_status %d %s (%s) in %.120s", (int)s_,     \
+                          rocsparse_get_status_name(s_),                                 \
+                          rocsparse_get_status_description(s_), #call);                  \
             g_err = m_;                                                                  \
             return kHip;                                                                 \
         }                                                                                \

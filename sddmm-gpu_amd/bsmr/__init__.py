@@ -44,7 +44,7 @@ class Tuning(C.Structure):
                 ("piece_weight", C.c_float), ("shard_piece_weight", C.c_float),
                 ("dense_min", C.c_float), ("orig_rows", C.c_int32), ("orig_contig", C.c_int32),
                 ("dense_ks", C.c_int32), ("dense_ns", C.c_int32), ("out_staged", C.c_int32),
-                ("l2_range_kb", C.c_int32)]
+                ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -126,7 +126,8 @@ EXPORTS = [
     "bsmr_plan_options_default", "bsmr_plan_create", "bsmr_plan_recolumn",
     "bsmr_plan_destroy", "bsmr_plan_get_stats", "bsmr_plan_get_array", "bsmr_plan_evaluate",
     "bsmr_sddmm", "bsmr_sddmm_batch", "bsmr_plan_shard", "bsmr_plan_shard_dtype",
-    "bsmr_shard_cuts", "bsmr_sddmm_panels", "bsmr_sddmm_panels_local",
+    "bsmr_shard_cuts", "bsmr_plan_shard_rebalance", "bsmr_sddmm_panels",
+    "bsmr_sddmm_panels_local",
     "bsmr_plan_export_rows", "bsmr_plan_import_rows",
     "bsmr_sddmm_profile", "bsmr_sddmm_cpu", "bsmr_check_one", "bsmr_check_data",
 ]
@@ -186,6 +187,7 @@ def lib():
     L.bsmr_plan_shard_dtype.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, C.c_int,
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.bsmr_shard_cuts.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_int, _u32p]
+    L.bsmr_plan_shard_rebalance.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, _u32p, _f32p, _u32p]
     L.bsmr_sddmm_panels.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
                                     C.c_uint32, vp]
     L.bsmr_sddmm_panels_local.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
@@ -230,7 +232,7 @@ def tuning_from_env(env=None):
         v = env.get(TUNING_ENV[f])
         if v is None:
             continue
-        if f in ("orig_rows", "out_staged"):  # tri-state: "0" never, "1" always, else auto
+        if f in ("orig_rows", "out_staged", "stage_nt"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
         elif f in ("piece_weight", "shard_piece_weight", "dense_min"):
             out[f] = float(v)
@@ -431,6 +433,18 @@ class Plan:
         _check(lib().bsmr_plan_shard_dtype(self.h, K, dtype, rank, world, C.byref(p0),
                                            C.byref(p1)), "bsmr_plan_shard_dtype")
         return p0.value, p1.value
+
+    def shard_rebalance(self, K, world, prev_cuts, shard_ms, dtype=F32):
+        """Cuts [0 = c_0 <= ... <= c_world = P] re-balanced by measured shard times
+        (bsmr_plan_shard_rebalance); prev_cuts: the cuts those times were measured on."""
+        prev = np.ascontiguousarray(prev_cuts, np.uint32)
+        ms = np.ascontiguousarray(shard_ms, np.float32)
+        if len(prev) != world + 1 or len(ms) != world:
+            raise ValueError("shard_rebalance: prev_cuts needs world + 1 entries, shard_ms world")
+        cuts = np.zeros(world + 1, np.uint32)
+        _check(lib().bsmr_plan_shard_rebalance(self.h, K, dtype, world, prev, ms, cuts),
+               "bsmr_plan_shard_rebalance")
+        return [int(c) for c in cuts]
 
     def profile(self, dA, dB, K, dP, iters=10, stream=0, dtype=F32):
         d, r, t = C.c_float(), C.c_float(), C.c_float()

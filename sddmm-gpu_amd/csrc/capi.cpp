@@ -29,6 +29,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->piece_weight = t->shard_piece_weight = t->dense_min = -1.0f;
     t->orig_rows = t->orig_contig = t->dense_ks = t->dense_ns = t->out_staged = -1;
     t->l2_range_kb = -1;
+    t->stage_nt = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -69,6 +70,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     geti("BSMR_DENSE_NS", t->dense_ns);
     get3("BSMR_OUT_STAGED", t->out_staged);
     geti("BSMR_L2_RANGE_KB", t->l2_range_kb);
+    get3("BSMR_STAGE_NT", t->stage_nt);
     return n;
 }
 
@@ -115,6 +117,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->dense_ks >= 0) p.dense_ks = t->dense_ks;
         if (t->dense_ns >= 0) p.dense_ns = t->dense_ns;
         if (t->out_staged >= 0) p.out_staged = t->out_staged ? 1 : 0;
+        if (t->stage_nt >= 0) p.stage_nt = t->stage_nt ? 1 : 0;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -475,6 +478,70 @@ extern "C" int bsmr_plan_shard(const bsmr_plan* plan, uint32_t K, int rank, int 
     return bsmr_plan_shard_dtype(plan, K, BSMR_F32, rank, world, p0, p1);
 }
 
+namespace {
+// cut [0, nRB) row blocks of cumulative cost cum (size nRB + 1) into `world` contiguous ranges,
+// each cut at the row-block boundary closest to its target; cuts are panel indices
+void cut_row_blocks(const std::vector<double>& cum, u32 nRB, u32 ppr, u32 P, int world, u32* cuts) {
+    cuts[0] = 0;
+    for (int r = 1; r < world; ++r) {
+        const double target = cum[nRB] * r / world;
+        u32 b = static_cast<u32>(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        if (b > 0 && target - cum[b - 1] < cum[std::min(b, nRB)] - target) --b;
+        cuts[r] = std::max(cuts[r - 1], std::min(b * ppr, P));
+    }
+    cuts[world] = P;
+}
+}  // namespace
+
+extern "C" int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int dtype, int world,
+                                         const uint32_t* prev_cuts, const float* shard_ms,
+                                         uint32_t* cuts) {
+    if (!plan || world <= 0 || !prev_cuts || !shard_ms || !cuts || K == 0 || K % 16 ||
+        (dtype != BSMR_F32 && dtype != BSMR_F16 && dtype != BSMR_BF16)) {
+        set_error("bsmr_plan_shard_rebalance: bad arguments");
+        return BSMR_ERR_INVALID;
+    }
+    const Plan& p = plan->p;
+    const Plan::RowBlockLayout* L = nullptr;
+    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
+    if (!L || L->nRB == 0 || L->orig) {
+        set_error("bsmr_plan_shard_rebalance: needs the row-block launch of the reordered plan");
+        return BSMR_ERR_UNSUPPORTED;
+    }
+    const u32 nRB = L->nRB, ppr = L->RB / 16;
+    if (prev_cuts[0] != 0 || prev_cuts[world] != p.P) {
+        set_error("bsmr_plan_shard_rebalance: previous cuts must span [0, P]");
+        return BSMR_ERR_INVALID;
+    }
+    // each row block's model cost scaled by its shard's measured / predicted time
+    std::vector<double> scale(nRB, 1.0);
+    for (int r = 0; r < world; ++r) {
+        if (prev_cuts[r + 1] < prev_cuts[r] || (prev_cuts[r] % ppr && prev_cuts[r] != p.P)) {
+            set_error("bsmr_plan_shard_rebalance: previous cuts are not row-block boundaries");
+            return BSMR_ERR_INVALID;
+        }
+        const u32 b0 = prev_cuts[r] / ppr, b1 = std::min(nRB, (prev_cuts[r + 1] + ppr - 1) / ppr);
+        double pred = 0.0;
+        for (u32 b = b0; b < b1; ++b) pred += L->rbCost[b];
+        if (pred <= 0.0 || !(shard_ms[r] > 0.0f)) continue;
+        const double f = static_cast<double>(shard_ms[r]) / pred;
+        for (u32 b = b0; b < b1; ++b) scale[b] = f;
+    }
+    // normalise the factors of measured shards to their mean, so unmeasured blocks keep weight 1
+    double fs = 0.0;
+    u32 nf = 0;
+    for (u32 b = 0; b < nRB; ++b)
+        if (scale[b] != 1.0) {
+            fs += scale[b];
+            ++nf;
+        }
+    const double norm = nf ? fs / nf : 1.0;
+    std::vector<double> cum(nRB + 1ull, 0.0);
+    for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b] * (scale[b] / norm);
+    cut_row_blocks(cum, nRB, ppr, p.P, world, cuts);
+    return BSMR_OK;
+}
+
 extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtype, int rank,
                                      int world, uint32_t* p0, uint32_t* p1) {
     if (!plan || world <= 0 || rank < 0 || rank >= world || !p0 || !p1 || K == 0 || K % 16 ||
@@ -493,15 +560,7 @@ extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtyp
         const u32 nRB = L->nRB, ppr = L->RB / 16;
         std::vector<double> cum(nRB + 1ull, 0.0);
         for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b];
-        cuts[0] = 0;
-        for (int r = 1; r < world; ++r) {
-            const double target = cum[nRB] * r / world;
-            // the boundary closest to the target
-            u32 b = static_cast<u32>(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-            if (b > 0 && target - cum[b - 1] < cum[std::min(b, nRB)] - target) --b;
-            cuts[r] = std::max(cuts[r - 1], std::min(b * ppr, p.P));
-        }
-        cuts[world] = p.P;
+        cut_row_blocks(cum, nRB, ppr, p.P, world, cuts.data());
     } else {
         BSMR_CHECK(bsmr_shard_cuts(p.h_blockOffsets.data(), p.h_sparseValueOffsets.data(), p.P, K,
                                    world, cuts.data()));

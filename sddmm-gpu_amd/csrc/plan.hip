@@ -125,6 +125,17 @@ __global__ void k_count_zero(const u32* __restrict__ sorted, u32 M, u32* out) {
 
 // state[pos] = ASSIGNED|0 for empty rows (cluster 0, rowReordering.cu:939-949), else 0 =
 // "rejected by virtual cluster 0"; st[0] = z + 1 so cluster 1 scans from position z.
+// per position of the ascending order: {encoding offset, #blocks, SC, S1C} of its row, so the
+// clustering reads a candidate's metadata in one 16-byte load instead of asc -> row -> 4 loads
+__global__ void k_pmeta(const u32* asc, const u32* rowptr, const u32* nblk, const u32* SC,
+                        const u32* S1C, u32 M, uint4* pmeta) {
+    const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < M) {
+        const u32 row = asc[p];
+        pmeta[p] = make_uint4(rowptr[row], nblk[row], SC[row], S1C[row]);
+    }
+}
+
 __global__ void k_init_state(u32* state, u32* st, u32 M, u32 z) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < M) state[i] = i < z ? ASSIGNED : 0u;
@@ -158,12 +169,8 @@ __global__ void k_init_state(u32* state, u32* st, u32 M, u32 z) {
 // the exact fp32 emulation below decides.
 // ------------------------------------------------------------------------------------------
 struct ClusterArgs {
-    const u32* asc;
-    const u32* rowptr;  // encoding offsets (= CSR row offsets)
-    const u32* nblk;
+    const uint4* pmeta;  // per position: encoding offset (= CSR row offset), #blocks, SC, S1C
     const u32* enc;
-    const u32* SC;
-    const u32* S1C;
     u32* state;
     u32* st;
     u32* ctrl;          // [0] abort, [1] timeout, [2..3] exact evals (u64), [4..5] total evals,
@@ -184,6 +191,8 @@ constexpr u32 CL_LDS_BUDGET = 148 * 1024;  // representatives (the control block
 // accept chains the leader resolves alone (re-evaluating one position at a time) before it
 // hands the rest of a sub-batch back to all waves
 constexpr u32 CL_LEADER_EVALS = 16;
+// encoding chunks (256 entries) of a row whose loads are issued together (registers: 4 per chunk)
+constexpr u32 CL_PRE_CH = 2;
 
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -196,6 +205,7 @@ struct ClusterCtl {
     float nr[CL_TMAX];     // sqrtf(SR)
     u32 SR[CL_TMAX];       // kept-block sum of squares of the representative (u32 wrap)
     u64 S1R[CL_TMAX];      // kept-block sum of the representative
+    u32 scanL[CL_WIN / 64], scanN[CL_WIN / 64];  // window scan: ready prefix, unassigned count
     u32 ntodo, t, nact, done, i, nact_eval;
     u64 nexact, ntotal;
 };
@@ -304,15 +314,9 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
 #pragma unroll
         for (u32 c = 0; c < TS; ++c) inr[c] = C.inrf[c];
         const float incf = 1.0f / nc;
-        u32 ent[4] = {pre[0], pre[1], pre[2], pre[3]};
-        for (u32 e0 = l; e0 < nb; e0 += 256) {
-            if (e0 != l) {
-#pragma unroll
-                for (u32 u = 0; u < 4; ++u) {
-                    const u32 e = e0 + 64 * u;
-                    ent[u] = e < nb ? a.enc[b0 + e] : 0u;
-                }
-            }
+        // one chunk of 4 entries per lane (entries l + 64u): fp32 minima summed over the chunk
+        auto chunk = [&](const u32 e0, const u32 e1, const u32 e2, const u32 e3) {
+            const u32 ent[4] = {e0, e1, e2, e3};
             float s[TS];
 #pragma unroll
             for (u32 c = 0; c < TS; ++c) s[c] = 0.0f;
@@ -348,6 +352,29 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
             }
 #pragma unroll
             for (u32 c = 0; c < TS; ++c) mn[c] += static_cast<double>(s[c]);
+        };
+        // the row's first CL_PRE_CH chunks: chunk 0 was prefetched (pre), the next ones are all
+        // issued now, so such a row pays one load round trip instead of one per chunk
+        // (T = 8 keeps chunk 0 only: its 8 representatives' partial sums fill the registers)
+        constexpr u32 NX = TS <= 6 ? 4 * (CL_PRE_CH - 1) : 0;
+        u32 ent[NX > 0 ? NX : 1];
+#pragma unroll
+        for (u32 u = 0; u < NX; ++u) {
+            const u32 e = l + 256 + 64 * u;
+            ent[u] = e < nb ? a.enc[b0 + e] : 0u;
+        }
+        chunk(pre[0], pre[1], pre[2], pre[3]);
+#pragma unroll
+        for (u32 q = 0; q < NX / 4; ++q)
+            if (256 * (q + 1) < nb) chunk(ent[4 * q], ent[4 * q + 1], ent[4 * q + 2], ent[4 * q + 3]);
+        for (u32 e0 = l + 256 + 64 * NX; e0 < nb; e0 += 256) {  // longer rows
+            u32 x[4];
+#pragma unroll
+            for (u32 u = 0; u < 4; ++u) {
+                const u32 e = e0 + 64 * u;
+                x[u] = e < nb ? a.enc[b0 + e] : 0u;
+            }
+            chunk(x[0], x[1], x[2], x[3]);
         }
         red = wave_sum8(mn);
     }
@@ -478,10 +505,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         return sim > a.alpha;
     };
-    auto row_meta = [&](u32 p) -> uint4 {
-        const u32 row = a.asc[p];
-        return make_uint4(a.rowptr[row], a.nblk[row], a.SC[row], a.S1C[row]);
-    };
+    auto row_meta = [&](u32 p) -> uint4 { return a.pmeta[p]; };
 
     // ---- leader: wait for the predecessor tile's last start, find the first cluster's start
     if (w == 0) {
@@ -547,29 +571,52 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
     u64 t_idle = now_ticks();
     while (!C.done) {
         __syncthreads();  // every wave has read the previous window's control words
-        // ---- leader: next window of ready positions (rejected by the predecessor tile or
-        // assigned); the unassigned ones and their rows' metadata go to C.todo / C.meta
+        // ---- next window of ready positions (rejected by the predecessor tile or assigned):
+        // the longest ready prefix of [C.i, C.i + CL_WIN), read by CL_WIN / 64 waves at once
+        // (state word and metadata of every position in one round trip); the unassigned ones and
+        // their rows' metadata go to C.todo / C.meta in position order
+        constexpr u32 SW = CL_WIN / 64;  // scanning waves
+        u32 sc_idx = 0;
+        uint4 sc_m = make_uint4(0, 0, 0, 0);
+        u64 sc_mm = 0;
+        if (w < SW) {
+            sc_idx = C.i + 64 * w + l;
+            const bool in = sc_idx < M;
+            const u32 v = in ? ld_agent(&a.state[sc_idx]) : ASSIGNED;
+            if (in) sc_m = row_meta(sc_idx);
+            const bool ready = (v & ASSIGNED) || v == pred;
+            const u64 notready = __ballot(!ready || !in);
+            const u32 L = notready ? __builtin_ctzll(notready) : 64u;
+            sc_mm = __ballot(!(v & ASSIGNED) && l < L);
+            if (l == 0) {
+                C.scanL[w] = L;
+                C.scanN[w] = static_cast<u32>(__builtin_popcountll(sc_mm));
+            }
+        }
+        __syncthreads();
+        if (w < SW) {
+            // wave w's chunk counts when every chunk before it was fully ready
+            u32 n0 = 0;
+            bool live = true;
+            for (u32 k = 0; k < w; ++k) {
+                live = live && C.scanL[k] == 64u;
+                n0 += C.scanN[k];
+            }
+            if (live && ((sc_mm >> l) & 1ull)) {
+                const u32 slot = n0 + __builtin_amdgcn_mbcnt_hi(
+                                          static_cast<u32>(sc_mm >> 32),
+                                          __builtin_amdgcn_mbcnt_lo(static_cast<u32>(sc_mm), 0u));
+                C.todo[slot] = sc_idx;
+                C.meta[slot] = sc_m;
+            }
+        }
         if (w == 0) {
-            u32 i = C.i, n = 0, total = 0;
-            bool stop = false;
-            while (!stop && total < CL_WIN && i + total < M) {
-                const u32 idx = i + total + l;
-                const u32 v = idx < M ? ld_agent(&a.state[idx]) : ASSIGNED;
-                const bool ready = (v & ASSIGNED) || v == pred;
-                const u64 notready = __ballot(!ready || idx >= M);
-                const u32 L = notready ? __builtin_ctzll(notready) : 64u;
-                const bool mine = !(v & ASSIGNED) && l < L;
-                const u64 mm = __ballot(mine);
-                if (mine) {
-                    const u32 slot = n + __builtin_amdgcn_mbcnt_hi(
-                                             static_cast<u32>(mm >> 32),
-                                             __builtin_amdgcn_mbcnt_lo(static_cast<u32>(mm), 0u));
-                    C.todo[slot] = idx;
-                    C.meta[slot] = row_meta(idx);
-                }
-                n += __builtin_popcountll(mm);
-                total += L;
-                stop = L < 64;
+            const u32 i = C.i;
+            u32 n = 0, total = 0;
+            for (u32 k = 0; k < SW; ++k) {
+                n += C.scanN[k];
+                total += C.scanL[k];
+                if (C.scanL[k] < 64u) break;
             }
             bool aborted = false;
             if (total == 0 && i < M) {
@@ -1712,13 +1759,14 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     hipLaunchKernelGGL(k_init_state, dim3(grid_for(M, 256)), dim3(256), 0, s, state.data(), st.data(),
                        M, z);
     BSMR_HIP(hipGetLastError());
+    DevBuf<uint4> pmeta;
+    BSMR_CHECK(pmeta.alloc(M));
+    hipLaunchKernelGGL(k_pmeta, dim3(grid_for(M, 256)), dim3(256), 0, s, asc.data(), rowptr.data(),
+                       nblk.data(), SC.data(), S1C.data(), M, pmeta.data());
+    BSMR_HIP(hipGetLastError());
     ClusterArgs ca{};
-    ca.asc = asc.data();
-    ca.rowptr = rowptr.data();
-    ca.nblk = nblk.data();
+    ca.pmeta = pmeta.data();
     ca.enc = enc.data();
-    ca.SC = SC.data();
-    ca.S1C = S1C.data();
     ca.state = state.data();
     ca.st = st.data();
     ca.ctrl = ctrl.data();

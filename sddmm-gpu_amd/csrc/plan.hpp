@@ -69,6 +69,10 @@ struct Plan {
     // 1.394 -> 1.305 ms; C2 nips-like (3 MB, P stays in L2 and its scattered stores merge there)
     // 11.86 -> 12.60 us, so it stays on one store per entry
     int out_staged = -1;
+    // A staging with the nt cache policy (BSMR_STAGE_NT: 0 never, 1 always, else auto = staged
+    // output layouts when stage_nt_auto)
+    int stage_nt = -1;
+    bool stage_nt_auto = false;
     u64 out_staged_min = 8ull << 20;
     // fp16/bf16 patterns with at least this fraction of M x N stored run the dense-sampled
     // launch (whole 128 x 128 MFMA tiles; BSMR_DENSE_MIN; > 1 = never). Measured crossover

@@ -17,6 +17,7 @@
 // bsmr_sddmm_panels (row-panel shards) uses the panel-major residual items instead, with the
 // panel's A rows staged in LDS.
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <vector>
 
@@ -415,6 +416,7 @@ struct RbArgs {
     // in LDS; the entry metadata's low bits are then the slot, and the workgroup writes the slots
     // to P[sortedPos[itemEnt.x + t]] at the end
     u32 outLds;
+    u32 stageNt;  // 1: stage the A rows with the nt policy (Plan::stage_nt)
     const u32* sortedPos;
     const uint2* itemEnt;
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
@@ -788,7 +790,11 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     pc.len = 0;
     if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
     if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
-    {
+    // AUX: the LDS-DMA cache policy (0 default; 2 = nt, stream the A rows past the XCD's L2 so the
+    // B columns of the item's column range stay resident: large staged-output layouts, where an
+    // item's row block is not staged again on that XCD until the next range)
+    auto stage = [&](auto aux_tag) {
+        constexpr int AUX = decltype(aux_tag)::value;
         // the source chunk of lane l is the same in every block of the wave: x % NCH and
         // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
         const u32 x0 = 64 * ws + lane;
@@ -806,7 +812,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                 const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                                  (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                                 16, 0, 0);
+                                                 16, 0, AUX);
             }
         } else {
 #pragma unroll
@@ -815,10 +821,14 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                 const char* g = a.A + (static_cast<size_t>(src[i]) * RBY + coff);
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                                  (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                                 16, 0, 0);
+                                                 16, 0, AUX);
             }
         }
-    }
+    };
+    if (a.stageNt)
+        stage(std::integral_constant<int, 2>{});
+    else
+        stage(std::integral_constant<int, 0>{});
     if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
     if (tw < ntile) dt.loadB(a, 0, tb);
     // every LDS-DMA of the workgroup has landed before any wave reads the image or writes the
@@ -1012,6 +1022,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.meta = L.meta.data();
     a.out = L.out.data();
     a.outLds = (mode & 2) ? L.outLds : 0u;  // (dense-only profiling launches write no slots)
+    a.stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
     a.sortedPos = L.sortedPos.data();
     a.itemEnt = L.itemEnt.data();
     a.tilePanel = p.denseItems.data();

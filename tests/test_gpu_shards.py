@@ -219,3 +219,26 @@ def test_bench_sharded_rccl_one_rank():
         assert sc[split]["ms_per_step"] > 0
     assert sc["global"]["whole_plan_one_gpu"]["ms_per_step"] > 0
     assert sum(sc["global"]["shards"]["entries"]) == sc["nnz"]
+
+
+def test_shard_rebalance_moves_cuts_toward_measured_balance():
+    """bsmr_plan_shard_rebalance: cuts stay on row-block boundaries, span [0, P], do not move
+    when every shard took the same time per model cost, and shrink a shard that ran slow."""
+    M, N, rp, ci = synth.random_rows(4000, 6000, 60, seed=31, zipf=1.1)
+    K = 128
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    world = 4
+    P = plan.stats()["num_row_panels"]
+    cuts = [plan.shard(K, r, world)[0] for r in range(world)] + [P]
+    assert cuts[0] == 0 and all(a <= b for a, b in zip(cuts, cuts[1:]))
+    rb = plan.stats()["rb_rows"][2] // 16  # panels per row block (512-byte rows)
+    assert rb > 0 and all(c % rb == 0 or c == P for c in cuts)
+    same = plan.shard_rebalance(K, world, cuts, [1.0] * world)
+    # equal times on model-balanced shards: the cuts can only move by the rounding to row blocks
+    assert all(abs(a - b) <= rb for a, b in zip(same, cuts)) and same[0] == 0 and same[-1] == P
+    slow = plan.shard_rebalance(K, world, cuts, [2.0, 1.0, 1.0, 1.0])
+    assert slow[1] <= cuts[1] and slow[-1] == P
+    assert all(c % rb == 0 or c == P for c in slow)
+    assert all(a <= b for a, b in zip(slow, slow[1:]))
+    with pytest.raises(Exception):
+        plan.shard_rebalance(K, world, cuts[:-1] + [P - 1], [1.0] * world)

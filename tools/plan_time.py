@@ -37,7 +37,10 @@ def main():
         rows = plan.array("reorderedRows")
         same = None if ref is None else bool(np.array_equal(rows, ref))
         ref = rows if ref is None else ref
+        import hashlib
         out["runs"][b] = {"wall_s": round(wall, 3), "row_reorder_ms": round(st["row_reorder_ms"], 2),
+                          "rows_sha256": hashlib.sha256(rows.tobytes()).hexdigest()[:16],
+                          "lib": os.environ.get("BSMR_LIB_PATH", "in-tree"),
                           "col_reorder_ms": round(st["col_reorder_ms"], 2),
                           "num_clusters": st["num_clusters"],
                           "total_similarity_evals": st["total_similarity_evals"],

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--copies", type=int, default=1,
                     help="stack this many column-relabelled copies (bench.py's C2 weak scaling at "
                          "--gpus copies; synth.stack_copies) and shard over world = copies only")
+    ap.add_argument("--rebalance", type=int, default=0,
+                    help="rounds of measured-cost re-cutting (bsmr_plan_shard_rebalance, as "
+                         "bench.py's global split does) after the model's cut")
     ap.add_argument("--local", action="store_true",
                     help="also time bench.py --shard local: contiguous original row panels of equal "
                          "stored entries, each on its own BSMR plan")
@@ -92,15 +95,33 @@ def main():
     so = plan.array("sparseValueOffsets").astype(np.int64)
     for world in [int(w) for w in args.worlds.split(",")]:
         shards = [plan.shard(K, r, world, code) for r in range(world)]
-        dP.fill_(float("nan"))
-        ms = []
-        for p0, p1 in shards:
-            ms.append(timed(lambda: plan.sddmm_panels(dA.data_ptr(), dB.data_ptr(), K,
-                                                       dP.data_ptr(), p0, p1, stream=s,
-                                                       dtype=code)))
+        history = []
+        for it in range(args.rebalance + 1):
+            dP.fill_(float("nan"))
+            ms = []
+            for p0, p1 in shards:
+                ms.append(timed(lambda: plan.sddmm_panels(dA.data_ptr(), dB.data_ptr(), K,
+                                                           dP.data_ptr(), p0, p1, stream=s,
+                                                           dtype=code)))
+            history.append({"cuts": [a for a, _ in shards] + [shards[-1][1]],
+                            "shard_ms": [round(x, 5) for x in ms], "step_ms": round(max(ms), 5),
+                            "imbalance": round(max(ms) / (sum(ms) / len(ms)), 3)})
+            if it == args.rebalance or world == 1:
+                break
+            cuts = plan.shard_rebalance(K, world, history[-1]["cuts"], ms, code)
+            shards = list(zip(cuts[:-1], cuts[1:]))
+        best = min(range(len(history)), key=lambda i: history[i]["step_ms"])
+        if best != len(history) - 1:  # the outputs below come from the fastest cut
+            c = history[best]["cuts"]
+            shards = list(zip(c[:-1], c[1:]))
+            dP.fill_(float("nan"))
+            ms = [timed(lambda: plan.sddmm_panels(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+                                                  p0, p1, stream=s, dtype=code))
+                  for p0, p1 in shards]
         P = dP.cpu().numpy()
         slow = max(ms)
         out["worlds"][world] = {
+            "rebalance_history": history,
             "shards": shards, "shard_ms": [round(x, 5) for x in ms],
             "shard_tiles": [int(bo[b] - bo[a]) for a, b in shards],
             "shard_residual": [int(so[b] - so[a]) for a, b in shards],
