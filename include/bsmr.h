@@ -105,6 +105,13 @@ typedef struct {
                                   -1 = auto */
     int32_t stage_nt;          /* BSMR_STAGE_NT: row-block A staging with the nt cache policy, 0
                                   never, 1 always, -1 auto */
+    int32_t seg_items;         /* BSMR_SEG_ITEMS: 1 = one workgroup item per split (row block,
+                                  column range) segment, cut only to the staged-output capacity;
+                                  -1 = cost-apportioned chunks */
+    int32_t rb_rows;           /* BSMR_RB_ROWS: rows per row block of the row-block launch (a
+                                  multiple of 16 within 160 KiB of LDS); -1 = by the LDS budget */
+    int32_t late_b;            /* BSMR_LATE_B: 1 = row-block phase-0 B columns loaded after the
+                                  staging barrier instead of behind the LDS-DMAs; -1 = 0 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

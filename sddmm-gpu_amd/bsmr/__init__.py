@@ -44,7 +44,8 @@ class Tuning(C.Structure):
                 ("piece_weight", C.c_float), ("shard_piece_weight", C.c_float),
                 ("dense_min", C.c_float), ("orig_rows", C.c_int32), ("orig_contig", C.c_int32),
                 ("dense_ks", C.c_int32), ("dense_ns", C.c_int32), ("out_staged", C.c_int32),
-                ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32)]
+                ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32), ("seg_items", C.c_int32),
+                ("rb_rows", C.c_int32), ("late_b", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)

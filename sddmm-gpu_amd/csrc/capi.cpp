@@ -30,6 +30,9 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->orig_rows = t->orig_contig = t->dense_ks = t->dense_ns = t->out_staged = -1;
     t->l2_range_kb = -1;
     t->stage_nt = -1;
+    t->seg_items = -1;
+    t->rb_rows = -1;
+    t->late_b = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -71,6 +74,9 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     get3("BSMR_OUT_STAGED", t->out_staged);
     geti("BSMR_L2_RANGE_KB", t->l2_range_kb);
     get3("BSMR_STAGE_NT", t->stage_nt);
+    geti("BSMR_SEG_ITEMS", t->seg_items);
+    geti("BSMR_RB_ROWS", t->rb_rows);
+    geti("BSMR_LATE_B", t->late_b);
     return n;
 }
 
@@ -118,6 +124,9 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->dense_ns >= 0) p.dense_ns = t->dense_ns;
         if (t->out_staged >= 0) p.out_staged = t->out_staged ? 1 : 0;
         if (t->stage_nt >= 0) p.stage_nt = t->stage_nt ? 1 : 0;
+        if (t->seg_items >= 0) p.seg_items = t->seg_items;
+        if (t->rb_rows > 0) p.rb_rows_force = t->rb_rows;
+        if (t->late_b >= 0) p.late_b = t->late_b;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;

@@ -185,7 +185,10 @@ struct ClusterArgs {
 constexpr double GUARD = 1e-5;
 constexpr u32 CL_TMAX = 8;      // clusters per tile (register arrays)
 constexpr u32 CL_WAVES = 16;    // waves per tile workgroup
-constexpr u32 CL_SUB = 64;      // positions per evaluation sub-batch (4 per wave)
+#ifndef BSMR_CL_SUB
+#define BSMR_CL_SUB 64
+#endif
+constexpr u32 CL_SUB = BSMR_CL_SUB;  // positions per evaluation sub-batch (4 per wave)
 constexpr u32 CL_WIN = 256;     // ready positions per window
 constexpr u32 CL_LDS_BUDGET = 148 * 1024;  // representatives (the control block follows)
 // accept chains the leader resolves alone (re-evaluating one position at a time) before it
@@ -680,7 +683,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                         const u32 n = tend - j;
                         const u32 r = l < n ? C.res[j + l] : 0u;
                         const u64 ev = __ballot(l < n && (r != 0u || C.nact < T));
-                        const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : n;
+                        const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : min(n, 64u);  // (one wave: 64 at a time)
                         if (l < e) st_agent(&a.state[C.todo[j + l]], klast);
                         ntot += static_cast<u64>(e) * C.nact;
                         j += e;
@@ -1358,6 +1361,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             RBr = std::min(RBr, std::max<u32>(16, (rb + 15) / 16 * 16));
         }
     }
+    if (rb_rows_force > 0)  // tuning: rows per block (a multiple of 16 within the LDS budget)
+        RBr = std::min(rowblock_rows(rowBytes, 160, Rs),
+                       std::max<u32>(16, (static_cast<u32>(rb_rows_force) + 15) / 16 * 16));
     const u32 nRB = std::max<u32>(1, (Rs + RBr - 1) / RBr);
     const size_t lds = static_cast<size_t>(RBr) * rowBytes;
     const u32 NT = lds > 80 * 1024 ? 1024 : 512;
@@ -1557,7 +1563,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             for (u32 b = 0; b < nRB; ++b)
                 c[static_cast<size_t>(j) * nRB + b] =
                     split[b] ? cost[static_cast<size_t>(b) * NCR + x * m + j] : 0.0;
-        const std::vector<u32> nch = apportion(c, qEach);
+        // one_item_per_segment: every (row block, range) segment is one item (cut only to the
+        // staged-output capacity), so no A image is staged twice for one segment; the XCD lists
+        // then differ in length by their segment counts
+        u32 qx = qEach;
+        if (seg_items == 1) {
+            qx = 0;
+            for (double v : c) qx += v > 0;
+        }
+        const std::vector<u32> nch = apportion(c, qx);
         for (u32 j = 0; j < m; ++j)
             for (u32 b = 0; b < nRB; ++b) {
                 const size_t i = static_cast<size_t>(b) * NCR + x * m + j;

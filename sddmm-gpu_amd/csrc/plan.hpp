@@ -72,6 +72,10 @@ struct Plan {
     // A staging with the nt cache policy (BSMR_STAGE_NT: 0 never, 1 always, else auto = staged
     // output layouts when stage_nt_auto)
     int stage_nt = -1;
+    // BSMR_SEG_ITEMS: 1 = one item per split (row block, column range) segment
+    int seg_items = -1;
+    int rb_rows_force = -1;  // BSMR_RB_ROWS: rows per row block (tuning / experiments)
+    int late_b = -1;         // BSMR_LATE_B: 1 = phase-0 B loads after the staging barrier
     bool stage_nt_auto = false;
     u64 out_staged_min = 8ull << 20;
     // fp16/bf16 patterns with at least this fraction of M x N stored run the dense-sampled

@@ -417,6 +417,7 @@ struct RbArgs {
     // to P[sortedPos[itemEnt.x + t]] at the end
     u32 outLds;
     u32 stageNt;  // 1: stage the A rows with the nt policy (Plan::stage_nt)
+    u32 lateB;    // 1: phase-0 B columns / metadata loaded after the staging barrier (late_b)
     const u32* sortedPos;
     const uint2* itemEnt;
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
@@ -829,13 +830,22 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         stage(std::integral_constant<int, 2>{});
     else
         stage(std::integral_constant<int, 0>{});
-    if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
-    if (tw < ntile) dt.loadB(a, 0, tb);
+    // the phase-0 B columns and entry metadata: issued right behind the LDS-DMAs (so the
+    // barrier's wait covers them too), or with lateB after the barrier (the barrier then waits
+    // for the staging alone and the waves pay one load round trip before their first piece)
+    if (!a.lateB) {
+        if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
+        if (tw < ntile) dt.loadB(a, 0, tb);
+    }
     // every LDS-DMA of the workgroup has landed before any wave reads the image or writes the
     // staged-output slots (the blocks past the image land in the tail those slots use); explicit,
     // not left to the compiler's wait insertion at the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (a.lateB) {
+        if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
+        if (tw < ntile) dt.loadB(a, 0, tb);
+    }
     const unsigned long long tm = rtime(a.trace);
     if (a.diag & 8) {  // staging only
         trace_wave(a.trace, blockIdx.x * NW + w, t0, tm);
@@ -1023,6 +1033,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.out = L.out.data();
     a.outLds = (mode & 2) ? L.outLds : 0u;  // (dense-only profiling launches write no slots)
     a.stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
+    a.lateB = p.late_b == 1;
     a.sortedPos = L.sortedPos.data();
     a.itemEnt = L.itemEnt.data();
     a.tilePanel = p.denseItems.data();

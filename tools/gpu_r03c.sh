@@ -8,6 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*" >> "$OUT/steps.log"; }
+step plan_ab && timeout -k 10 600 bash tools/gpu_plan_ab.sh "$TAG/plan_ab" 0.5 "sub128 sub256" &&
 step ab_nt && timeout -k 10 900 bash tools/ab_env.sh "$TAG/ab_nt" BSMR_STAGE_NT "0 1 0 1" "C4x1 C4 C3 C2" &&
 step fetch_nt && BSMR_STAGE_NT=1 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_sddmm --output-format csv \
     -d "$OUT/fetch_nt" -o run -- python3 tools/prof_sddmm.py --iters 3 --workload reddit_like --scale 1.0 > "$OUT/fetch_nt.log" 2>&1 &&

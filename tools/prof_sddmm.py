@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
     ap.add_argument("--mask", default=None, help="dlmc_like mask: uniform | block")
     ap.add_argument("--diag", type=int, default=0, help="BSMR_DIAG ablation bits (sddmm.hip)")
+    ap.add_argument("--alpha", type=float, default=0.3)
+    ap.add_argument("--delta", type=float, default=0.3)
     args = ap.parse_args()
     if args.diag:
         os.environ["BSMR_DIAG"] = str(args.diag)
@@ -34,14 +36,17 @@ def main():
     import bsmr
     from bsmr import Plan, make_data, set_default_tuning, synth, tuning_from_env
 
-    gen = getattr(synth, args.workload)
+    if args.workload in synth.SUITESPARSE_REBUILDS:  # e.g. Trefethen_20000, mycielskian15
+        gen = synth.SUITESPARSE_REBUILDS[args.workload]
+    else:
+        gen = getattr(synth, args.workload)
     if args.mask is not None:
         M, N, rp, ci = gen(args.mask)
     else:
         M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
     K = args.K
     set_default_tuning(tuning_from_env())  # BSMR_* A/B knobs (the library reads no env)
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, layout=args.layout,
+    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, layout=args.layout,
                 lds_budget_kb=args.lds_kb)
     tdt = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}[args.dtype]
     code = {"f32": bsmr.F32, "f16": bsmr.F16, "bf16": bsmr.BF16}[args.dtype]
@@ -56,7 +61,8 @@ def main():
     st = plan.stats()
     print(json.dumps({"M": M, "N": N, "nnz": len(ci), "K": K, "dtype": args.dtype,
                       "workload": args.workload, "layout": args.layout,
-                      "rb": {k: st[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
+                      "rb": {k: st[k] for k in ("rb_rows", "rb_items", "rb_pieces", "rb_work_items",
+                                                "rb_orig_rows")},
                       "lds_kb": args.lds_kb, "timing_ms": r,
                       "dense_items": st["dense_items"], "residual_slots_hint": st["residual_items"],
                       "dense_tiles": st["num_dense_tiles"], "residual": st["num_residual"]}))
