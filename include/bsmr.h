@@ -111,7 +111,8 @@ typedef struct {
     int32_t rb_rows;           /* BSMR_RB_ROWS: rows per row block of the row-block launch (a
                                   multiple of 16 within 160 KiB of LDS); -1 = by the LDS budget */
     int32_t late_b;            /* BSMR_LATE_B: 1 = row-block phase-0 B columns loaded after the
-                                  staging barrier instead of behind the LDS-DMAs; -1 = 0 */
+                                  staging barrier instead of behind the LDS-DMAs (0 = behind them);
+                                  -1 = 1 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

@@ -75,7 +75,10 @@ struct Plan {
     // BSMR_SEG_ITEMS: 1 = one item per split (row block, column range) segment
     int seg_items = -1;
     int rb_rows_force = -1;  // BSMR_RB_ROWS: rows per row block (tuning / experiments)
-    int late_b = -1;         // BSMR_LATE_B: 1 = phase-0 B loads after the staging barrier
+    // BSMR_LATE_B: phase-0 B loads after the staging barrier (0 = behind the LDS-DMAs, else on).
+    // Measured (profiles/r03d/ab_lateb): C2 11.05 -> 10.86 us, C3 72.0 -> 68.9, C4 x0.5 1.012 ->
+    // 0.998 ms, C5 unchanged
+    int late_b = -1;
     bool stage_nt_auto = false;
     u64 out_staged_min = 8ull << 20;
     // fp16/bf16 patterns with at least this fraction of M x N stored run the dense-sampled

@@ -1033,7 +1033,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.out = L.out.data();
     a.outLds = (mode & 2) ? L.outLds : 0u;  // (dense-only profiling launches write no slots)
     a.stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
-    a.lateB = p.late_b == 1;
+    a.lateB = p.late_b != 0;
     a.sortedPos = L.sortedPos.data();
     a.itemEnt = L.itemEnt.data();
     a.tilePanel = p.denseItems.data();
