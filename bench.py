@@ -107,6 +107,14 @@ def workload(args):
         f"C5: dlmc_like 2048^2 90% sparse {args.mask} mask (seed 7), bf16 A/B, fp32 accumulate")
 
 
+def host_threads():
+    """Host threads for the CPU legs: OMP_NUM_THREADS (the box's CPU share) or all cores, capped
+    at 16 — a one-GPU box's share; os.cpu_count() there is the whole machine's, and a box has
+    been seen exporting OMP_NUM_THREADS=256, which oversubscribes a shared host."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    return max(1, min(16, n))
+
+
 def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
     """Oracle host SDDMM (host.cpp:45-76 restated), timed on this box's host cores."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -114,7 +122,7 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
 
     import oracle_lib as O
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = host_threads()
     c = O.CSR.from_arrays(M, N, rp, ci)
     lib = O.lib()
     Af = np.ascontiguousarray(A, np.float32)
@@ -397,7 +405,7 @@ def main_c1(args):
     M, N, rp, ci = synth.nips_like()
     K = args.K or 32
     nnz = len(ci)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = host_threads()
     A = make_data(M * K)
     B = make_data(N * K)
     sddmm_cpu(M, N, rp, ci, K, A, B, threads=threads)  # warm-up
@@ -661,8 +669,7 @@ def _host_ref(M, N, rp, ci, K, A, B, dtype, tdt):
     else:
         Ar = torch.from_numpy(A).to(tdt).float().numpy()
         Br = torch.from_numpy(B).to(tdt).float().numpy()
-    return sddmm_cpu(M, N, rp, ci, K, Ar, Br,
-                     threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    return sddmm_cpu(M, N, rp, ci, K, Ar, Br, threads=host_threads())
 
 
 def _bcast_b(B_host, N, K, tdt, dev):
@@ -737,6 +744,9 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
 
     def use(c):  # this rank's panels of cuts c and their A rows on the device
         cur["p0"], cur["p1"] = c[rank], c[rank + 1]
+        # outputs of the previous cut's panels would survive in this rank's P and be summed
+        # twice by the gather: every cut starts from a zeroed P
+        dP.zero_()
         A_local = D.shard_a_rows(A, K, rows, cur["p0"], cur["p1"])
         cur["dA"] = torch.from_numpy(A_local.reshape(-1)).to(dev).to(tdt)
         if cur["dA"].numel() == 0:

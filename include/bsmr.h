@@ -113,6 +113,14 @@ typedef struct {
     int32_t late_b;            /* BSMR_LATE_B: 1 = row-block phase-0 B columns loaded after the
                                   staging barrier instead of behind the LDS-DMAs (0 = behind them);
                                   -1 = 1 */
+    float item_cap;            /* BSMR_ITEM_CAP: no row-block item above this multiple of one
+                                  workgroup slot's share of the launch's cost (0 = no cap);
+                                  < 0 = 2 */
+    int32_t item_sched;        /* BSMR_ITEM_SCHED: 1 = chunk cuts by cost, unsplit items list-
+                                  scheduled heaviest first onto the XCD where they start earliest,
+                                  and sparse-row patterns with fewer row blocks than slots sized
+                                  to one block per slot; 0 = entry-even cuts, fewest-items deal,
+                                  LDS-budget blocks; -1 = 1 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

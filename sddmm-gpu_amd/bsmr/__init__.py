@@ -45,7 +45,8 @@ class Tuning(C.Structure):
                 ("dense_min", C.c_float), ("orig_rows", C.c_int32), ("orig_contig", C.c_int32),
                 ("dense_ks", C.c_int32), ("dense_ns", C.c_int32), ("out_staged", C.c_int32),
                 ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32), ("seg_items", C.c_int32),
-                ("rb_rows", C.c_int32), ("late_b", C.c_int32)]
+                ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
+                ("item_sched", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -233,9 +234,9 @@ def tuning_from_env(env=None):
         v = env.get(TUNING_ENV[f])
         if v is None:
             continue
-        if f in ("orig_rows", "out_staged", "stage_nt"):  # tri-state: "0" never, "1" always, else auto
+        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
-        elif f in ("piece_weight", "shard_piece_weight", "dense_min"):
+        elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap"):
             out[f] = float(v)
         else:
             out[f] = int(v)

@@ -33,6 +33,8 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->seg_items = -1;
     t->rb_rows = -1;
     t->late_b = -1;
+    t->item_cap = -1.0f;
+    t->item_sched = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -77,6 +79,8 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     geti("BSMR_SEG_ITEMS", t->seg_items);
     geti("BSMR_RB_ROWS", t->rb_rows);
     geti("BSMR_LATE_B", t->late_b);
+    getf("BSMR_ITEM_CAP", t->item_cap);
+    get3("BSMR_ITEM_SCHED", t->item_sched);
     return n;
 }
 
@@ -127,6 +131,9 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->seg_items >= 0) p.seg_items = t->seg_items;
         if (t->rb_rows > 0) p.rb_rows_force = t->rb_rows;
         if (t->late_b >= 0) p.late_b = t->late_b;
+        if (t->item_cap >= 0) p.item_cap = t->item_cap;
+        if (t->item_sched >= 0)
+            p.item_cost_cuts = p.item_lpt = p.small_sparse_rb = t->item_sched != 0;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;

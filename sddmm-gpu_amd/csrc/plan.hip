@@ -17,7 +17,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <queue>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -1249,8 +1251,9 @@ u32 rowblock_rows(u32 rowBytes, u32 lds_kb, u32 R) {
 }
 
 namespace {
-// split q chunks over segments by cost (largest remainder); every non-empty segment gets >= 1
-std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
+// split q chunks over segments by cost (largest remainder); every non-empty segment gets >= 1,
+// and >= ceil(cost / cap) when cap > 0 (no chunk above cap; the total may then exceed q)
+std::vector<u32> apportion(const std::vector<double>& cost, u32 q, double cap = 0.0) {
     const size_t n = cost.size();
     std::vector<u32> out(n, 0);
     double tot = 0;
@@ -1262,8 +1265,9 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q) {
         if (cost[i] <= 0) continue;
         const double ideal = q * cost[i] / tot;
         out[i] = std::max<u32>(1, static_cast<u32>(std::floor(ideal)));
+        if (cap > 0) out[i] = std::max<u32>(out[i], static_cast<u32>(std::ceil(cost[i] / cap)));
         used += out[i];
-        frac.push_back({ideal - std::floor(ideal), i});
+        frac.push_back({ideal - out[i], i});
     }
     std::stable_sort(frac.begin(), frac.end(),
                      [](const auto& a, const auto& b) { return a.first > b.first; });
@@ -1344,7 +1348,12 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 n0 = orig ? nnz : h_sparseValueOffsets[pb] - ebase;
     // staged output (results through LDS, written per item in CSR order) for large P
     const bool stagedWanted = out_staged == 1 || (out_staged == -1 && 4ull * nnz > out_staged_min);
-    const u32 ldsKb = stagedWanted && !rb_lds_user ? rb_lds_kb_staged : rb_lds_kb;
+    // staged-output budget by row size (item_sched): 1 KiB rows take an 80 KiB image (two
+    // workgroups per CU, results stored directly), 2 KiB rows the whole 160 KiB (mycielskian K =
+    // 256 / 512: 379 -> 358 us and 896 -> 771 us against the 120 KiB staged image;
+    // profiles/r03f/itemcal); 512-byte rows keep the tuned 120 KiB staged image (C4)
+    const u32 stagedKb = !item_cost_cuts || rowBytes <= 512 ? rb_lds_kb_staged : rowBytes <= 1024 ? 80u : 160u;
+    const u32 ldsKb = stagedWanted && !rb_lds_user ? stagedKb : rb_lds_kb;
     const u32 l2Kb = stagedWanted && !l2_range_user ? l2_range_kb_staged : l2_range_kb;
     u32 RBr = rowblock_rows(rowBytes, ldsKb, Rs);
     {
@@ -1359,6 +1368,16 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             const u32 rounds = (nRB0 + slots - 1) / slots;
             const u32 rb = (Rs + rounds * slots - 1) / (rounds * slots);
             RBr = std::min(RBr, std::max<u32>(16, (rb + 15) / 16 * 16));
+        } else if (Rs && n0 < 64ull * Rs && small_sparse_rb) {
+            // fewer row blocks than slots: a block would be cut into chunks that each restage
+            // its whole image for a few entries (Trefethen_20000 K = 64: 35 blocks of 576 rows in
+            // 257 items, 15.2 us). One block per slot instead, at two workgroups per CU when the
+            // image fits 80 KiB (48-row blocks in 512 items: 8.9 us; profiles/r03e/itemcal)
+            const u32 s2 = static_cast<u32>(cus) * 2u;
+            const u32 rb2 = std::max<u32>(16, ((Rs + s2 - 1) / s2 + 15) / 16 * 16);
+            const u32 rb1 = std::max<u32>(16, ((Rs + cus - 1) / cus + 15) / 16 * 16);
+            if (static_cast<size_t>(rb2) * rowBytes <= 80 * 1024) RBr = std::min(RBr, rb2);
+            else RBr = std::min(RBr, rb1);
         }
     }
     if (rb_rows_force > 0)  // tuning: rows per block (a multiple of 16 within the LDS budget)
@@ -1455,12 +1474,27 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     std::vector<u32> cuts(NCR + 1, N);
     cuts[0] = 0;
     {
-        std::vector<u32> cnt(N + 1, 0);
-        for (u32 i = 0; i < n; ++i) ++cnt[hmeta[i] & CM];
-        u64 run = 0;
+        // column weight: its entries, plus (item_sched) piece_weight per column-run piece it
+        // heads, so the XCDs' ranges carry equal modeled cost rather than equal entry counts
+        // (mycielskian: the last XCD's range carried 10 % more piece work and ended 10 % later)
+        std::vector<double> cnt(N + 1, 0.0);
+        for (u32 b = 0, lo = 0; b < nRB; ++b) {
+            const u32 hi = rbEnd[b];
+            u32 run = 0;
+            for (u32 i = lo; i < hi; ++i) {
+                const u32 c = hmeta[i] & CM;
+                const bool start = i == lo || c != (hmeta[i - 1] & CM) || run >= piece_max;
+                run = start ? 1 : run + 1;
+                cnt[c] += 1.0 + (item_cost_cuts && start ? piece_weight : 0.0);
+            }
+            lo = std::max(lo, hi);
+        }
+        double tot = 0;
+        for (u32 c = 0; c < N; ++c) tot += cnt[c];
+        double run = 0;
         u32 x = 1;
         for (u32 c = 0; c < N && x < NCR; ++c) {
-            while (x < NCR && run >= static_cast<u64>(n) * x / NCR) cuts[x++] = c;
+            while (x < NCR && run >= tot * x / NCR) cuts[x++] = c;
             run += cnt[c];
         }
         for (; x < NCR; ++x) cuts[x] = N;
@@ -1516,6 +1550,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 Q1 = perBucket * XCD_BUCKETS;
     u32 Q = std::max<u32>(1, std::min<u32>(Q1, static_cast<u32>(total / 128.0)));
     const double target = total / Q;
+    // no chunk above item_cap x one slot's share of a round (0: off): a row block of one hub row
+    // (mycielskian: 8 K single-entry pieces in one item against a 6 K-entry median) otherwise
+    // outlasts the whole launch (profiles/r03e/itemcal). 1x would force extra items into a
+    // second round wherever a segment sits just above the mean (C2: 11 -> 17 us)
+    const double cap = item_cap > 0 ? item_cap * total / Q1 : 0.0;
     std::vector<double> cb(nRB, 0.0);
     std::vector<char> split(nRB, 0);
     double splitTotal = 0;
@@ -1538,17 +1577,64 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 qSplit = qEach * XCD_BUCKETS;
     std::vector<double> cu(nRB, 0.0);
     for (u32 b = 0; b < nRB; ++b) cu[b] = split[b] ? 0.0 : cb[b];
-    const std::vector<u32> nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u);
+    const std::vector<u32> nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u, cap);
+    if (diag & 1024) {  // layout debug (host stderr)
+        std::fprintf(stderr, "[rb layout] RB %u NT %u nRB %u m %u Q1 %u Q %u total %.0f target %.0f cap %.0f "
+                     "splitTotal %.0f qEach %u segMax %u\n", RBr, NT, nRB, m, Q1, Q, total, target, cap,
+                     splitTotal, qEach, segMax);
+        for (u32 b = 0; b < nRB; ++b)
+            if (cb[b] > 2 * target)
+                std::fprintf(stderr, "[rb layout]   block %u cost %.0f split %d nu %u\n", b, cb[b], split[b], nu[b]);
+    }
     // staged output: the LDS past the A image (the launch takes 160 / 80 KiB) holds an item's
     // results when it has room for >= 1024 of them; larger items are cut to fit
     const size_t ldsDyn = (NT == 1024 ? 160u : 80u) * 1024u;
     const u32 outCap = ldsDyn > lds ? static_cast<u32>((ldsDyn - lds) / 4) : 0u;
     const bool staged = stagedWanted && outCap >= 1024;
+    // chunk k of an entry range: cut where the running cost (1 per entry + piece_weight per
+    // column-run piece start) crosses k / nch of the range's cost, so chunks of single-entry
+    // pieces get fewer entries than chunks of long runs; a chunk above the staged-output
+    // capacity is then cut entry-evenly into as many as it needs (an entry-even cut of the whole
+    // range would put a hub row's single-entry run into one chunk of 5x the others' cost)
+    std::vector<u32> ecut, ecut2;
+    auto cuts_by_cost = [&](u32 e0, u32 ne, u32 nch) {
+        ecut.assign(nch + 1, e0 + ne);
+        ecut[0] = e0;
+        if (nch <= 1 || !item_cost_cuts) {
+            for (u32 k = 1; k < nch; ++k) ecut[k] = e0 + static_cast<u32>(static_cast<u64>(ne) * k / nch);
+            return;
+        }
+        double tot = 0;
+        u32 run = 0;
+        for (u32 e = e0; e < e0 + ne; ++e) {
+            const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+            run = start ? 1 : run + 1;
+            tot += 1.0 + (start ? piece_weight : 0.0);
+        }
+        double acc = 0;
+        u32 k = 1;
+        run = 0;
+        for (u32 e = e0; e < e0 + ne && k < nch; ++e) {
+            const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+            run = start ? 1 : run + 1;
+            while (k < nch && acc >= tot * k / nch) ecut[k++] = e;
+            acc += 1.0 + (start ? piece_weight : 0.0);
+        }
+        if (!staged) return;
+        ecut2.assign(1, e0);
+        for (u32 j = 0; j < nch; ++j) {
+            const u32 a = ecut[j], len = ecut[j + 1] - a, parts = std::max<u32>(1, (len + outCap - 1) / outCap);
+            for (u32 q = 1; q <= parts; ++q) ecut2.push_back(a + static_cast<u32>(static_cast<u64>(len) * q / parts));
+        }
+        ecut.swap(ecut2);
+    };
     auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch) {
         if (staged) nch = std::max<u32>(nch, (ne + outCap - 1) / outCap);
+        cuts_by_cost(e0, ne, nch);
+        nch = static_cast<u32>(ecut.size() - 1);
         for (u32 k = 0; k < nch; ++k) {
-            const u32 ea = e0 + static_cast<u32>(static_cast<u64>(ne) * k / nch);
-            const u32 eb = e0 + static_cast<u32>(static_cast<u64>(ne) * (k + 1) / nch);
+            const u32 ea = ecut[k];
+            const u32 eb = ecut[k + 1];
             const u32 ta = t0 + static_cast<u32>(static_cast<u64>(nt) * k / nch);
             const u32 tb = t0 + static_cast<u32>(static_cast<u64>(nt) * (k + 1) / nch);
             if (ea == eb && ta == tb) continue;
@@ -1571,7 +1657,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             qx = 0;
             for (double v : c) qx += v > 0;
         }
-        const std::vector<u32> nch = apportion(c, qx);
+        const std::vector<u32> nch = apportion(c, qx, seg_items == 1 ? 0.0 : cap);
         for (u32 j = 0; j < m; ++j)
             for (u32 b = 0; b < nRB; ++b) {
                 const size_t i = static_cast<size_t>(b) * NCR + x * m + j;
@@ -1592,16 +1678,60 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     }
     {
         const size_t nsp = lists[spare].size();
-        for (size_t next = 0; next < nsp; ++next) {
-            u32 x = 0;  // the list with the fewest items (ties: lowest index)
-            for (u32 y = 1; y < XCD_BUCKETS; ++y)
-                if (lists[y].size() < lists[x].size()) x = y;
-            // original-order blocks (orig_contig): XCD x takes the x-th contiguous eighth, so the
-            // band's B rows of neighbouring blocks stay in one L2
-            if (orig && orig_contig && qSplit == 0)
-                x = static_cast<u32>(next * XCD_BUCKETS / nsp);
-            lists[x].push_back(lists[spare][next]);
-            lends[x].push_back(lends[spare][next]);
+        const bool contig = orig && orig_contig && qSplit == 0;
+        if (item_lpt && !contig && nsp) {
+            // list scheduling: each XCD runs its list on perBucket slots, an item starting when a
+            // slot frees (in list order). The XCD lists' split items are simulated first; then
+            // the unsplit items, heaviest first, each go to the XCD where it starts earliest
+            // (ties: fewer items, lower index), appended to that list, which keeps every list in
+            // descending order of its unsplit items' cost
+            auto icost = [&](const uint4& it, u32 eb) {
+                double c = (eb - it.w) + 16.0 * (it.z - it.y) + piece_weight * RBr + item_fixed;
+                u32 run = 0;
+                for (u32 e = it.w; e < eb; ++e) {
+                    const bool start = e == it.w || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+                    run = start ? 1 : run + 1;
+                    c += start ? piece_weight : 0.0;
+                }
+                return c;
+            };
+            using Slot = std::priority_queue<double, std::vector<double>, std::greater<double>>;
+            std::vector<Slot> free(XCD_BUCKETS);
+            for (u32 x = 0; x < XCD_BUCKETS; ++x) {
+                for (u32 k = 0; k < perBucket; ++k) free[x].push(0.0);
+                for (size_t j = 0; j < lists[x].size(); ++j) {
+                    const double t = free[x].top();
+                    free[x].pop();
+                    free[x].push(t + icost(lists[x][j], lends[x][j]));
+                }
+            }
+            std::vector<std::pair<double, size_t>> ord(nsp);
+            for (size_t i = 0; i < nsp; ++i) ord[i] = {icost(lists[spare][i], lends[spare][i]), i};
+            std::stable_sort(ord.begin(), ord.end(),
+                             [](const auto& a, const auto& b) { return a.first > b.first; });
+            for (const auto& [c, i] : ord) {
+                u32 x = 0;
+                for (u32 y = 1; y < XCD_BUCKETS; ++y) {
+                    const double ty = free[y].top(), tx = free[x].top();
+                    if (ty < tx || (ty == tx && lists[y].size() < lists[x].size())) x = y;
+                }
+                const double t = free[x].top();
+                free[x].pop();
+                free[x].push(t + c);
+                lists[x].push_back(lists[spare][i]);
+                lends[x].push_back(lends[spare][i]);
+            }
+        } else {
+            for (size_t next = 0; next < nsp; ++next) {
+                u32 x = 0;  // the list with the fewest items (ties: lowest index)
+                for (u32 y = 1; y < XCD_BUCKETS; ++y)
+                    if (lists[y].size() < lists[x].size()) x = y;
+                // original-order blocks (orig_contig): XCD x takes the x-th contiguous eighth, so
+                // the band's B rows of neighbouring blocks stay in one L2
+                if (contig) x = static_cast<u32>(next * XCD_BUCKETS / nsp);
+                lists[x].push_back(lists[spare][next]);
+                lends[x].push_back(lends[spare][next]);
+            }
         }
         lists.resize(XCD_BUCKETS);
         lends.resize(XCD_BUCKETS);
@@ -1649,12 +1779,14 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     }
     L.rbCost.assign(nRB, 0.0);
     L.nWorkItems = 0;
+    L.itemStat.assign(items.size(), make_uint4(0, 0, 0, 0));
     for (size_t i = 0; i < items.size(); ++i) {
         const uint4 it = items[i];
         if (it.y == it.z && it.w == ends[i]) continue;  // padding
         ++L.nWorkItems;
         u64 ent = 0;
         for (u32 k = it.w; k < ends[i]; ++k) ent += (pieces[k].y >> 22) + 1;
+        L.itemStat[i] = make_uint4(it.x, it.z - it.y, static_cast<u32>(ent), ends[i] - it.w);
         L.rbCost[it.x] += static_cast<double>(ent) + shard_piece_weight * (ends[i] - it.w) +
                           16.0 * (it.z - it.y) + RBr;
     }

@@ -79,6 +79,14 @@ struct Plan {
     // Measured (profiles/r03d/ab_lateb): C2 11.05 -> 10.86 us, C3 72.0 -> 68.9, C4 x0.5 1.012 ->
     // 0.998 ms, C5 unchanged
     int late_b = -1;
+    // item cost cap (multiple of one slot's share of a round; 0 = none), cost-even chunk cuts and
+    // list-scheduled (heaviest-first) unsplit items; item_fixed = an item's fixed cost in entries
+    // beside its staged rows (piece_weight each). BSMR_ITEM_CAP / BSMR_ITEM_SCHED
+    double item_cap = 2.0;
+    bool item_cost_cuts = true, item_lpt = true;
+    double item_fixed = 1024.0;
+    // sparse-row patterns with fewer row blocks than slots: one block per workgroup slot
+    bool small_sparse_rb = true;
     bool stage_nt_auto = false;
     u64 out_staged_min = 8ull << 20;
     // fp16/bf16 patterns with at least this fraction of M x N stored run the dense-sampled
@@ -156,6 +164,8 @@ struct Plan {
         // per row block: Σ over its items of (entries + pieces + 16 tiles + RB staged rows), the
         // shard cost model of bsmr_plan_shard
         std::vector<double> rbCost;
+        // per item slot (launch order): {row block, kept tiles, entries, pieces}; padding zeros
+        std::vector<uint4> itemStat;
         // original-order row blocks (banded / FEM patterns whose reordering scatters the band):
         // row block b = original rows [b RB, (b + 1) RB), staged through rowIds (identity), every
         // entry residual; whole-plan launches only (shards cut reordered panels)

@@ -1301,6 +1301,37 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     return BSMR_OK;
 }
 
+// debug: the whole-plan row-block layout of (K, dtype), 4 u32 per item slot in launch order
+// {row block, kept tiles, entries, pieces} (padding slots all zero), preceded by the header
+// {rows per block, threads per workgroup, items, row bytes}; *len = 4 (items + 1). Not in the
+// header (tools/item_trace.py)
+extern "C" int bsmr_debug_rb_items(const bsmr_plan* plan, uint32_t K, int dtype, uint32_t* host_out,
+                                   uint64_t* len) {
+    if (!plan) return BSMR_ERR_INVALID;
+    const Plan& p = plan->p;
+    const Plan::RowBlockLayout* L = nullptr;
+    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
+    if (!L) {
+        if (len) *len = 0;
+        return BSMR_OK;
+    }
+    if (len) *len = 4ull * (L->itemStat.size() + 1);
+    if (host_out) {
+        host_out[0] = L->RB;
+        host_out[1] = L->NT;
+        host_out[2] = static_cast<uint32_t>(L->itemStat.size());
+        host_out[3] = L->rowBytes;
+        for (size_t i = 0; i < L->itemStat.size(); ++i) {
+            const uint4 v = L->itemStat[i];
+            host_out[4 * (i + 1) + 0] = v.x;
+            host_out[4 * (i + 1) + 1] = v.y;
+            host_out[4 * (i + 1) + 2] = v.z;
+            host_out[4 * (i + 1) + 3] = v.w;
+        }
+    }
+    return BSMR_OK;
+}
+
 // debug timeline of the last traced launch (BSMR_DIAG & 32): 4 u64 per wave (not in the header)
 extern "C" int bsmr_debug_trace(const bsmr_plan* plan, uint64_t* host_out, uint64_t* len) {
     if (!plan) return BSMR_ERR_INVALID;

@@ -112,9 +112,9 @@ def retime_and_cpu(M, N, rp, ci, K, alpha, delta, iters=100):
     nnz = len(ci)
     flops = 2.0 * nnz * K
     bytes_alg = 4.0 * K * (M + N) + 8.0 * nnz + 4.0 * (M + 1)
-    # the box's CPU share (OMP_NUM_THREADS is set to it on the GPU box; all of os.cpu_count()
-    # would oversubscribe a shared host)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    # the box's CPU share: at most 16 threads (a box has exported OMP_NUM_THREADS=256, and all of
+    # os.cpu_count() would oversubscribe a shared host)
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
     sddmm_cpu(M, N, rp, ci, K, A, B, threads=threads)
     ts = []
     for _ in range(3):
