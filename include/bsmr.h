@@ -115,7 +115,8 @@ typedef struct {
                                   -1 = 1 */
     float item_cap;            /* BSMR_ITEM_CAP: no row-block item above this multiple of one
                                   workgroup slot's share of the launch's cost (0 = no cap);
-                                  < 0 = 2 */
+                                  < 0 = auto: the multiple in {2, 1.5, 1.25, 1} whose item
+                                  lists a slot model runs fastest */
     int32_t item_sched;        /* BSMR_ITEM_SCHED: 1 = chunk cuts by cost, unsplit items list-
                                   scheduled heaviest first onto the XCD where they start earliest,
                                   and sparse-row patterns with fewer row blocks than slots sized

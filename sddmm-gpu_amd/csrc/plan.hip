@@ -182,6 +182,11 @@ struct ClusterArgs {
     float alpha;
     int exact_all;
     u64 timeout_ticks;  // s_memrealtime ticks (100 MHz)
+    // BSMR_DIAG & 2048: per tile (global index (first cluster - 1) / T) 12 u64: kernel entry,
+    // start found, end (s_memrealtime), windows, empty windows, sub-batch rounds, evaluations,
+    // ticket, ticks in window scans (spins included), in evaluation, in the leader's resolution;
+    // else null
+    unsigned long long* ctrace;
 };
 
 constexpr double GUARD = 1e-5;
@@ -213,6 +218,9 @@ struct ClusterCtl {
     u32 scanL[CL_WIN / 64], scanN[CL_WIN / 64];  // window scan: ready prefix, unassigned count
     u32 ntodo, t, nact, done, i, nact_eval;
     u64 nexact, ntotal;
+    u64 tr_begin, tr_started;  // BSMR_DIAG & 2048 timeline (ClusterArgs::ctrace)
+    u64 tr_t0, tr_scan, tr_eval, tr_lead;
+    u32 tr_win, tr_idle, tr_sub;
 };
 
 // exact fp32 similarity of a tile cluster (LDS, element i at rep[i * TS]) with the row whose
@@ -430,6 +438,12 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
     __shared__ u32 s_ticket;
     if (tid == 0) s_ticket = atomicAdd(&a.ctrl[6], 1u);
     for (u32 x = tid; x < a.NP * TS; x += blockDim.x) reps[x] = 0;
+    if (tid == 0) {
+        C.tr_begin = a.ctrace ? now_ticks() : 0ull;
+        C.tr_started = 0;
+        C.tr_scan = C.tr_eval = C.tr_lead = 0;
+        C.tr_win = C.tr_idle = C.tr_sub = 0;
+    }
     if (tid < CL_TMAX) {
         C.inrf[tid] = 0.0f;
         C.nr[tid] = 0.0f;
@@ -569,6 +583,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
             const uint4 m = row_meta(start);
             new_cluster(start, m);
         }
+        if (a.ctrace && l == 0) C.tr_started = now_ticks();
         if (aborted && l == 0) C.nact = T;  // no ST_NONE on abort: the host reports the timeout
     }
     __syncthreads();
@@ -576,6 +591,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
     u64 t_idle = now_ticks();
     while (!C.done) {
         __syncthreads();  // every wave has read the previous window's control words
+        if (a.ctrace && tid == 0) C.tr_t0 = now_ticks();
         // ---- next window of ready positions (rejected by the predecessor tile or assigned):
         // the longest ready prefix of [C.i, C.i + CL_WIN), read by CL_WIN / 64 waves at once
         // (state word and metadata of every position in one round trip); the unassigned ones and
@@ -624,7 +640,9 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                 if (C.scanL[k] < 64u) break;
             }
             bool aborted = false;
+            if (l == 0) ++C.tr_win;
             if (total == 0 && i < M) {
+                if (l == 0) ++C.tr_idle;
                 if (check_abort(t_idle)) aborted = true;
                 else __builtin_amdgcn_s_sleep(1);
             } else {
@@ -642,11 +660,16 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
             }
         }
         __syncthreads();
+        if (a.ctrace && tid == 0) C.tr_scan += now_ticks() - C.tr_t0;
         if (C.done && C.ntodo == 0) break;
         // ---- evaluate / resolve sub-batches
         while (true) {
             const u32 t = C.t, ntodo = C.ntodo, nact = C.nact;
             if (t >= ntodo) break;
+            if (tid == 0) {
+                ++C.tr_sub;
+                if (a.ctrace) C.tr_t0 = now_ticks();
+            }
             const u32 tend = min(ntodo, t + CL_SUB);
             {
                 u32 j = t + w;
@@ -670,6 +693,11 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                 }
             }
             __syncthreads();
+            if (a.ctrace && tid == 0) {
+                const u64 tn = now_ticks();
+                C.tr_eval += tn - C.tr_t0;
+                C.tr_t0 = tn;
+            }
             if (w == 0) {
                 // the sequential rule over the sub-batch. Verdicts of clusters whose
                 // representative changed since the evaluation (dirty: accepts, new clusters)
@@ -745,6 +773,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                 }
             }
             __syncthreads();
+            if (a.ctrace && tid == 0) C.tr_lead += now_ticks() - C.tr_t0;
         }
         if (C.done) break;
     }
@@ -752,6 +781,21 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
         for (u32 c = C.nact; c < T; ++c) st_agent(&a.st[kfirst + c], ST_NONE);
         atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[2]), C.nexact);
         atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[4]), C.ntotal);
+        if (a.ctrace) {
+            unsigned long long* tr = a.ctrace + 12ull * ((kfirst - 1) / T);
+            tr[0] = C.tr_begin;
+            tr[1] = C.tr_started;
+            tr[2] = now_ticks();
+            tr[3] = C.tr_win;
+            tr[4] = C.tr_idle;
+            tr[5] = C.tr_sub;
+            tr[6] = C.ntotal;
+            tr[7] = ticket;
+            tr[8] = C.tr_scan;
+            tr[9] = C.tr_eval;
+            tr[10] = C.tr_lead;
+            tr[11] = C.nexact;
+        }
     }
 }
 
@@ -1554,7 +1598,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // (mycielskian: 8 K single-entry pieces in one item against a 6 K-entry median) otherwise
     // outlasts the whole launch (profiles/r03e/itemcal). 1x would force extra items into a
     // second round wherever a segment sits just above the mean (C2: 11 -> 17 us)
-    const double cap = item_cap > 0 ? item_cap * total / Q1 : 0.0;
+    const double cap = (item_cap < 0 ? 2.0 : item_cap) * total / Q1;
     std::vector<double> cb(nRB, 0.0);
     std::vector<char> split(nRB, 0);
     double splitTotal = 0;
@@ -1577,15 +1621,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 qSplit = qEach * XCD_BUCKETS;
     std::vector<double> cu(nRB, 0.0);
     for (u32 b = 0; b < nRB; ++b) cu[b] = split[b] ? 0.0 : cb[b];
-    const std::vector<u32> nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u, cap);
-    if (diag & 1024) {  // layout debug (host stderr)
-        std::fprintf(stderr, "[rb layout] RB %u NT %u nRB %u m %u Q1 %u Q %u total %.0f target %.0f cap %.0f "
-                     "splitTotal %.0f qEach %u segMax %u\n", RBr, NT, nRB, m, Q1, Q, total, target, cap,
-                     splitTotal, qEach, segMax);
-        for (u32 b = 0; b < nRB; ++b)
-            if (cb[b] > 2 * target)
-                std::fprintf(stderr, "[rb layout]   block %u cost %.0f split %d nu %u\n", b, cb[b], split[b], nu[b]);
-    }
+    std::vector<u32> nu;
     // staged output: the LDS past the A image (the launch takes 160 / 80 KiB) holds an item's
     // results when it has room for >= 1024 of them; larger items are cut to fit
     const size_t ldsDyn = (NT == 1024 ? 160u : 80u) * 1024u;
@@ -1642,6 +1678,25 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             lends[xl].push_back(eb);
         }
     };
+    // modeled cost of an item (entries [it.w, eb)): entries + piece_weight per column-run piece
+    // + 16 per kept tile + its staging (piece_weight per row) + item_fixed
+    auto icost = [&](const uint4& it, u32 eb) {
+        double c = (eb - it.w) + 16.0 * (it.z - it.y) + piece_weight * RBr + item_fixed;
+        u32 run = 0;
+        for (u32 e = it.w; e < eb; ++e) {
+            const bool start = e == it.w || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+            run = start ? 1 : run + 1;
+            c += start ? piece_weight : 0.0;
+        }
+        return c;
+    };
+    using Slot = std::priority_queue<double, std::vector<double>, std::greater<double>>;
+    // the XCD lists for one cost cap (0: none); returns the modeled makespan: each XCD runs its
+    // list on perBucket slots, an item starting when a slot frees (in list order)
+    auto build_lists = [&](const double capv) -> double {
+    lists.assign(XCD_BUCKETS, {});
+    lends.assign(XCD_BUCKETS, {});
+    nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u, capv);
     for (u32 x = 0; x < XCD_BUCKETS; ++x) {
         // XCD x's segments in (range, row block) order
         std::vector<double> c(static_cast<size_t>(m) * nRB, 0.0);
@@ -1657,7 +1712,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             qx = 0;
             for (double v : c) qx += v > 0;
         }
-        const std::vector<u32> nch = apportion(c, qx, seg_items == 1 ? 0.0 : cap);
+        const std::vector<u32> nch = apportion(c, qx, seg_items == 1 ? 0.0 : capv);
         for (u32 j = 0; j < m; ++j)
             for (u32 b = 0; b < nRB; ++b) {
                 const size_t i = static_cast<size_t>(b) * NCR + x * m + j;
@@ -1685,17 +1740,6 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             // the unsplit items, heaviest first, each go to the XCD where it starts earliest
             // (ties: fewer items, lower index), appended to that list, which keeps every list in
             // descending order of its unsplit items' cost
-            auto icost = [&](const uint4& it, u32 eb) {
-                double c = (eb - it.w) + 16.0 * (it.z - it.y) + piece_weight * RBr + item_fixed;
-                u32 run = 0;
-                for (u32 e = it.w; e < eb; ++e) {
-                    const bool start = e == it.w || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
-                    run = start ? 1 : run + 1;
-                    c += start ? piece_weight : 0.0;
-                }
-                return c;
-            };
-            using Slot = std::priority_queue<double, std::vector<double>, std::greater<double>>;
             std::vector<Slot> free(XCD_BUCKETS);
             for (u32 x = 0; x < XCD_BUCKETS; ++x) {
                 for (u32 k = 0; k < perBucket; ++k) free[x].push(0.0);
@@ -1735,6 +1779,45 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         }
         lists.resize(XCD_BUCKETS);
         lends.resize(XCD_BUCKETS);
+    }
+    double ms = 0.0;
+    for (u32 x = 0; x < XCD_BUCKETS; ++x) {
+        Slot fr;
+        for (u32 k = 0; k < perBucket; ++k) fr.push(0.0);
+        double end = 0.0;
+        for (size_t j = 0; j < lists[x].size(); ++j) {
+            const double t = fr.top() + icost(lists[x][j], lends[x][j]);
+            fr.pop();
+            fr.push(t);
+            end = std::max(end, t);
+        }
+        ms = std::max(ms, end);
+    }
+    return ms;
+    };
+    // the cap: item_cap x one slot's share, or (auto, item_sched, up to 32 M entries) the
+    // multiple in {2, 1.5, 1.25, 1} whose lists the slot model runs fastest (a one-round launch
+    // ends with its longest item: mycielskian15 K = 256, 2x cap 144 us; C2's segments sit just
+    // above the mean, where 1x would open a second round)
+    double capUse = cap;
+    if (item_lpt && item_cap < 0 && n <= (1u << 25)) {
+        double best = -1.0;
+        for (const double f : {2.0, 1.5, 1.25, 1.0}) {
+            const double msf = build_lists(f * total / Q1);
+            if (best < 0 || msf < 0.995 * best) {
+                best = msf;
+                capUse = f * total / Q1;
+            }
+        }
+    }
+    const double msUse = build_lists(capUse);
+    if (diag & 1024) {  // layout debug (host stderr)
+        std::fprintf(stderr, "[rb layout] RB %u NT %u nRB %u m %u Q1 %u Q %u total %.0f target %.0f cap %.0f (used %.0f, model makespan %.0f) "
+                     "splitTotal %.0f qEach %u segMax %u\n", RBr, NT, nRB, m, Q1, Q, total, target, cap, capUse, msUse,
+                     splitTotal, qEach, segMax);
+        for (u32 b = 0; b < nRB; ++b)
+            if (cb[b] > 2 * target)
+                std::fprintf(stderr, "[rb layout]   block %u cost %.0f split %d nu %u\n", b, cb[b], split[b], nu[b]);
     }
     size_t nmax = 0;
     for (const auto& l : lists) nmax = std::max(nmax, l.size());
@@ -1941,6 +2024,11 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     BSMR_CHECK(cmpScratch.alloc(static_cast<size_t>(tilesMax) * nbpr));
     BSMR_HIP(hipMemsetAsync(cmpScratch.data(), 0, static_cast<size_t>(tilesMax) * nbpr * sizeof(u32), s));
     ca.cmpScratch = cmpScratch.data();
+    ca.ctrace = nullptr;
+    if (diag & 2048) {  // clustering timeline (tools/cluster_trace.py): 12 u64 per tile
+        BSMR_CHECK(prepare_trace((static_cast<size_t>(M) / T + 2) * 3, s));
+        ca.ctrace = trace.data();
+    }
     u32 c0 = 1;
     u32 last_valid = 0;
     while (c0 <= M) {  // at most M - z clusters

@@ -82,7 +82,7 @@ struct Plan {
     // item cost cap (multiple of one slot's share of a round; 0 = none), cost-even chunk cuts and
     // list-scheduled (heaviest-first) unsplit items; item_fixed = an item's fixed cost in entries
     // beside its staged rows (piece_weight each). BSMR_ITEM_CAP / BSMR_ITEM_SCHED
-    double item_cap = 2.0;
+    double item_cap = -1.0;  // < 0: auto (build_rowblock_layout), 0: no cap
     bool item_cost_cuts = true, item_lpt = true;
     double item_fixed = 1024.0;
     // sparse-row patterns with fewer row blocks than slots: one block per workgroup slot
