@@ -305,6 +305,41 @@ __device__ __forceinline__ double wave_sum8(const double (&v)[CL_TMAX]) {
     return s;
 }
 
+// verdict bits of tile clusters [0, nact) on the row with metadata m (see eval_row), from the
+// estimate's min-sum of cluster c (mnc_of(c); only read when est)
+template <class F>
+__device__ __forceinline__ u32 cl_verdict(const ClusterArgs& a, const ClusterCtl& C, uint4 m,
+                                          u32 nact, bool est, F mnc_of) {
+    const u32 scr = m.z, s1c = m.w;
+    const float nc = sqrtf(static_cast<float>(scr));
+    u32 acc = 0, ex = 0;
+    for (u32 c = 0; c < nact; ++c) {
+        const u32 SR = C.SR[c];
+        if (SR == 0 && scr == 0) {
+            if (1.0f > a.alpha) acc |= 1u << c;
+            continue;
+        }
+        if (SR == 0 || scr == 0) {
+            if (0.0f > a.alpha) acc |= 1u << c;
+            continue;
+        }
+        if (!est) {
+            ex |= 1u << c;
+            continue;
+        }
+        const double mnc = mnc_of(c);
+        const double mx = static_cast<double>(C.S1R[c]) / C.nr[c] + static_cast<double>(s1c) / nc - mnc;
+        const double sim = mnc / mx;
+        const double ad = static_cast<double>(a.alpha);
+        if (fabs(sim - ad) > GUARD) {
+            if (sim > ad) acc |= 1u << c;
+        } else {
+            ex |= 1u << c;
+        }
+    }
+    return acc | (ex << 8);
+}
+
 // one wave: the verdicts of tile clusters [0, nact) on the row with metadata m (encoding offset,
 // #blocks, SC, S1C) and first encoding chunk pre (entries l + 64u, 0 past the row), from the
 // estimate: bit c of the low byte = accept, of the second byte = guard band (the exact emulation
@@ -391,32 +426,8 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
         }
         red = wave_sum8(mn);
     }
-    u32 acc = 0, ex = 0;
-    for (u32 c = 0; c < nact; ++c) {
-        const u32 SR = C.SR[c];
-        if (SR == 0 && scr == 0) {
-            if (1.0f > a.alpha) acc |= 1u << c;
-            continue;
-        }
-        if (SR == 0 || scr == 0) {
-            if (0.0f > a.alpha) acc |= 1u << c;
-            continue;
-        }
-        if (!est) {
-            ex |= 1u << c;
-            continue;
-        }
-        const double mnc = readlane_f64(red, 8 * c);
-        const double mx = static_cast<double>(C.S1R[c]) / C.nr[c] + static_cast<double>(s1c) / nc - mnc;
-        const double sim = mnc / mx;
-        const double ad = static_cast<double>(a.alpha);
-        if (fabs(sim - ad) > GUARD) {
-            if (sim > ad) acc |= 1u << c;
-        } else {
-            ex |= 1u << c;
-        }
-    }
-    return acc | (ex << 8);
+    (void)s1c;
+    return cl_verdict(a, C, m, nact, est, [&](u32 c) { return readlane_f64(red, 8 * c); });
 }
 
 __device__ __forceinline__ void load_chunk0(const ClusterArgs& a, uint4 m, u32 (&ent)[4]) {
@@ -1633,40 +1644,53 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // capacity is then cut entry-evenly into as many as it needs (an entry-even cut of the whole
     // range would put a hub row's single-entry run into one chunk of 5x the others' cost)
     std::vector<u32> ecut, ecut2;
-    auto cuts_by_cost = [&](u32 e0, u32 ne, u32 nch) {
+    // tot = the range's entries + piece_weight per piece (known from its segments' costs), so
+    // one pass finds the cuts; ccost = the chunks' costs (entries + pieces) for the slot model
+    std::vector<double> ccost, ccost2;
+    auto cuts_by_cost = [&](u32 e0, u32 ne, u32 nch, double tot) {
         ecut.assign(nch + 1, e0 + ne);
         ecut[0] = e0;
-        if (nch <= 1 || !item_cost_cuts) {
+        ccost.assign(nch, nch ? tot / nch : 0.0);
+        if (nch > 1 && !item_cost_cuts) {
             for (u32 k = 1; k < nch; ++k) ecut[k] = e0 + static_cast<u32>(static_cast<u64>(ne) * k / nch);
-            return;
-        }
-        double tot = 0;
-        u32 run = 0;
-        for (u32 e = e0; e < e0 + ne; ++e) {
-            const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
-            run = start ? 1 : run + 1;
-            tot += 1.0 + (start ? piece_weight : 0.0);
-        }
-        double acc = 0;
-        u32 k = 1;
-        run = 0;
-        for (u32 e = e0; e < e0 + ne && k < nch; ++e) {
-            const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
-            run = start ? 1 : run + 1;
-            while (k < nch && acc >= tot * k / nch) ecut[k++] = e;
-            acc += 1.0 + (start ? piece_weight : 0.0);
+        } else if (nch > 1) {
+            double acc = 0, last = 0;
+            u32 k = 1, run = 0;
+            for (u32 e = e0; e < e0 + ne && k < nch; ++e) {
+                const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+                run = start ? 1 : run + 1;
+                while (k < nch && acc >= tot * k / nch) {
+                    ecut[k] = e;
+                    ccost[k - 1] = acc - last;
+                    last = acc;
+                    ++k;
+                }
+                acc += 1.0 + (start ? piece_weight : 0.0);
+            }
+            // the chunk from the last cut runs to the range's end; cuts never reached (k < nch)
+            // leave empty chunks behind it
+            for (u32 j = k; j < nch; ++j) ccost[j] = 0.0;
+            ccost[k - 1] = std::max(0.0, tot - last);
         }
         if (!staged) return;
         ecut2.assign(1, e0);
+        ccost2.clear();
         for (u32 j = 0; j < nch; ++j) {
             const u32 a = ecut[j], len = ecut[j + 1] - a, parts = std::max<u32>(1, (len + outCap - 1) / outCap);
-            for (u32 q = 1; q <= parts; ++q) ecut2.push_back(a + static_cast<u32>(static_cast<u64>(len) * q / parts));
+            for (u32 q = 1; q <= parts; ++q) {
+                ecut2.push_back(a + static_cast<u32>(static_cast<u64>(len) * q / parts));
+                ccost2.push_back(ccost[j] / parts);
+            }
         }
         ecut.swap(ecut2);
+        ccost.swap(ccost2);
     };
-    auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch) {
+    // lcost: each item's modeled cost (its entries + pieces + 16 per kept tile + staging
+    // (piece_weight per row) + item_fixed), for the slot model
+    std::vector<std::vector<double>> lcost(XCD_BUCKETS);
+    auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch, double rcost) {
         if (staged) nch = std::max<u32>(nch, (ne + outCap - 1) / outCap);
-        cuts_by_cost(e0, ne, nch);
+        cuts_by_cost(e0, ne, nch, rcost);
         nch = static_cast<u32>(ecut.size() - 1);
         for (u32 k = 0; k < nch; ++k) {
             const u32 ea = ecut[k];
@@ -1676,19 +1700,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             if (ea == eb && ta == tb) continue;
             lists[xl].push_back(make_uint4(b, ta, tb, ea));
             lends[xl].push_back(eb);
+            lcost[xl].push_back(ccost[k] + 16.0 * (tb - ta) + piece_weight * RBr + item_fixed);
         }
-    };
-    // modeled cost of an item (entries [it.w, eb)): entries + piece_weight per column-run piece
-    // + 16 per kept tile + its staging (piece_weight per row) + item_fixed
-    auto icost = [&](const uint4& it, u32 eb) {
-        double c = (eb - it.w) + 16.0 * (it.z - it.y) + piece_weight * RBr + item_fixed;
-        u32 run = 0;
-        for (u32 e = it.w; e < eb; ++e) {
-            const bool start = e == it.w || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
-            run = start ? 1 : run + 1;
-            c += start ? piece_weight : 0.0;
-        }
-        return c;
     };
     using Slot = std::priority_queue<double, std::vector<double>, std::greater<double>>;
     // the XCD lists for one cost cap (0: none); returns the modeled makespan: each XCD runs its
@@ -1696,6 +1709,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     auto build_lists = [&](const double capv) -> double {
     lists.assign(XCD_BUCKETS, {});
     lends.assign(XCD_BUCKETS, {});
+    lcost.assign(XCD_BUCKETS, {});
     nu = apportion(cu, Q > qSplit ? Q - qSplit : 0u, capv);
     for (u32 x = 0; x < XCD_BUCKETS; ++x) {
         // XCD x's segments in (range, row block) order
@@ -1717,7 +1731,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             for (u32 b = 0; b < nRB; ++b) {
                 const size_t i = static_cast<size_t>(b) * NCR + x * m + j;
                 const u32 q = nch[static_cast<size_t>(j) * nRB + b];
-                if (q) emit(x, b, se0[i], se1[i] - se0[i], st0[i], st1[i] - st0[i], q);
+                if (q)
+                    emit(x, b, se0[i], se1[i] - se0[i], st0[i], st1[i] - st0[i], q,
+                         (se1[i] - se0[i]) + piece_weight * spc[i]);
             }
     }
     // unsplit row blocks: their items, in row-block order, go to the list with the fewest items,
@@ -1726,10 +1742,13 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 spare = XCD_BUCKETS;  // staging list index
     lists.resize(XCD_BUCKETS + 1);
     lends.resize(XCD_BUCKETS + 1);
+    lcost.resize(XCD_BUCKETS + 1);
     for (u32 b = 0; b < nRB; ++b) {
         if (!nu[b]) continue;
         const size_t i0 = static_cast<size_t>(b) * NCR, i1 = i0 + NCR - 1;
-        emit(spare, b, se0[i0], se1[i1] - se0[i0], st0[i0], st1[i1] - st0[i0], nu[b]);
+        double rc = 0.0;
+        for (size_t i = i0; i <= i1; ++i) rc += (se1[i] - se0[i]) + piece_weight * spc[i];
+        emit(spare, b, se0[i0], se1[i1] - se0[i0], st0[i0], st1[i1] - st0[i0], nu[b], rc);
     }
     {
         const size_t nsp = lists[spare].size();
@@ -1746,11 +1765,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                 for (size_t j = 0; j < lists[x].size(); ++j) {
                     const double t = free[x].top();
                     free[x].pop();
-                    free[x].push(t + icost(lists[x][j], lends[x][j]));
+                    free[x].push(t + lcost[x][j]);
                 }
             }
             std::vector<std::pair<double, size_t>> ord(nsp);
-            for (size_t i = 0; i < nsp; ++i) ord[i] = {icost(lists[spare][i], lends[spare][i]), i};
+            for (size_t i = 0; i < nsp; ++i) ord[i] = {lcost[spare][i], i};
             std::stable_sort(ord.begin(), ord.end(),
                              [](const auto& a, const auto& b) { return a.first > b.first; });
             for (const auto& [c, i] : ord) {
@@ -1764,6 +1783,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                 free[x].push(t + c);
                 lists[x].push_back(lists[spare][i]);
                 lends[x].push_back(lends[spare][i]);
+                lcost[x].push_back(c);
             }
         } else {
             for (size_t next = 0; next < nsp; ++next) {
@@ -1775,10 +1795,12 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                 if (contig) x = static_cast<u32>(next * XCD_BUCKETS / nsp);
                 lists[x].push_back(lists[spare][next]);
                 lends[x].push_back(lends[spare][next]);
+                lcost[x].push_back(lcost[spare][next]);
             }
         }
         lists.resize(XCD_BUCKETS);
         lends.resize(XCD_BUCKETS);
+        lcost.resize(XCD_BUCKETS);
     }
     double ms = 0.0;
     for (u32 x = 0; x < XCD_BUCKETS; ++x) {
@@ -1786,7 +1808,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         for (u32 k = 0; k < perBucket; ++k) fr.push(0.0);
         double end = 0.0;
         for (size_t j = 0; j < lists[x].size(); ++j) {
-            const double t = fr.top() + icost(lists[x][j], lends[x][j]);
+            const double t = fr.top() + lcost[x][j];
             fr.pop();
             fr.push(t);
             end = std::max(end, t);

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-3: clustering by row groups of 4 waves — plan exactness tests, plan-time A/B against the
+# one-wave-per-row build (lib_clold), the chain timeline at reddit-like x1, and the item
+# scheduling A/B + C4 x1 first-call layout time after the one-pass chunk costs
+set -o pipefail
+TAG=${1:-r03i}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() { echo "[$(date +%T)] $*" >> "$OUT/steps.log"; }
+step tests && timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 &&
+step plan_ab_half && timeout -k 10 600 bash tools/gpu_plan_ab.sh "$TAG/plan_ab" 0.5 "clold" &&
+step plan_ab_x1 && timeout -k 10 600 bash tools/gpu_plan_ab.sh "$TAG/plan_ab" 1.0 "clold" &&
+step cltrace && timeout -k 10 300 python3 tools/cluster_trace.py --workload reddit_like --scale 1.0 > "$OUT/cltrace_x1.json" 2> "$OUT/cltrace_x1.err" &&
+step ab_sched && timeout -k 10 900 bash tools/ab_sched.sh "$TAG/ab_sched" "C2 C4 M15 M16k512 T64" &&
+step shards && timeout -k 10 600 python3 tools/shard_sim.py --workload reddit_like --scale 1.0 --worlds 8 > "$OUT/shards_c4x1.json" 2> "$OUT/shards_c4x1.err"
+rc=$?
+step "done rc=$rc"
+echo "rc=$rc" > "$OUT/rc.txt"
+exit $rc
