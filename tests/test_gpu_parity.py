@@ -242,6 +242,14 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     ({"BSMR_OUT_STAGED": "1", "BSMR_TILE_MIN_HALF": "0"}, 512, 2),
     ({"BSMR_OUT_STAGED": "1", "BSMR_ORIG_ROWS": "1"}, 128, 0),
     ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "64", "BSMR_TILE_MIN_F32": "0"}, 64, 0),
+    # item scheduling: the round-2 layout, fixed caps, and one with staged output
+    ({"BSMR_ITEM_SCHED": "0", "BSMR_ITEM_CAP": "0"}, 128, 0),
+    ({"BSMR_ITEM_CAP": "1"}, 128, 0),
+    ({"BSMR_ITEM_CAP": "1.25", "BSMR_OUT_STAGED": "1"}, 256, 1),
+    ({"BSMR_ITEM_SCHED": "0"}, 512, 2),
+    ({"BSMR_LATE_B": "0"}, 128, 0),
+    ({"BSMR_RB_ROWS": "16"}, 128, 0),
+    ({"BSMR_RB_ROWS": "48", "BSMR_OUT_STAGED": "1"}, 512, 0),
 ])
 def test_rowblock_layout_variants(env, K, dtype):
     """Launch-layout switches (tile demotion thresholds, L2 column ranges, piece order) on the

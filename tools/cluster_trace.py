@@ -45,7 +45,7 @@ def main():
     L.bsmr_debug_trace(plan.h, None, C.byref(n))
     buf = np.zeros(n.value, np.uint64)
     L.bsmr_debug_trace(plan.h, buf.ctypes.data, C.byref(n))
-    t = buf.reshape(-1, 12)
+    t = buf.reshape(-1, 16)
     t = t[t[:, 2] > 0].astype(np.int64)
     if args.dump:
         np.save(args.dump, t)
@@ -76,6 +76,11 @@ def main():
                           for k, i in (("scan_and_spin", 8), ("evaluate", 9), ("leader", 10))},
            "eval_us_per_subbatch": round(float(t[:, 9].sum() * us / max(1, t[:, 5].sum())), 2),
            "lead_us_per_subbatch": round(float(t[:, 10].sum() * us / max(1, t[:, 5].sum())), 2),
+           # wave 0's own rows against the whole evaluation phase (the rest: waiting at the
+           # barrier for slower waves), and its encoding entries per row / per microsecond
+           "wave0_own_frac_of_eval": round(float(t[:, 12].sum() / max(1, t[:, 9].sum())), 3),
+           "wave0_entries_per_subbatch": round(float(t[:, 13].sum() / max(1, t[:, 5].sum())), 1),
+           "wave0_entries_per_us": round(float(t[:, 13].sum() / max(1e-9, t[:, 12].sum() * us)), 1),
            "alive": {"p10": int(np.percentile(alive, 10)), "p50": int(np.median(alive)),
                      "max": int(max(alive))},
            "first_launches": launches[:3]}
