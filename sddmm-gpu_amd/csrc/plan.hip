@@ -179,13 +179,15 @@ struct ClusterArgs {
                         // [6] the launch's tile ticket counter
     u32* cmpScratch;    // [tiles][nbpr] zeros: dense row image of the exact path
     u32 M, nbpr, NP, B, keptMask, c0, T;
+    u32 allKept;  // every warp of the reduction tree kept (B / 32 a power of two): no kept test
     float alpha;
     int exact_all;
     u64 timeout_ticks;  // s_memrealtime ticks (100 MHz)
-    // BSMR_DIAG & 2048: per tile (global index (first cluster - 1) / T) 12 u64: kernel entry,
+    // BSMR_DIAG & 2048: per tile (global index (first cluster - 1) / T) 16 u64: kernel entry,
     // start found, end (s_memrealtime), windows, empty windows, sub-batch rounds, evaluations,
-    // ticket, ticks in window scans (spins included), in evaluation, in the leader's resolution;
-    // else null
+    // ticket, ticks in window scans (spins included), in evaluation, in the leader's resolution,
+    // exact evaluations, ticks wave 0 spent on its own rows, encoding entries wave 0 read; else
+    // null
     unsigned long long* ctrace;
 };
 
@@ -217,9 +219,10 @@ struct ClusterCtl {
     u64 S1R[CL_TMAX];      // kept-block sum of the representative
     u32 scanL[CL_WIN / 64], scanN[CL_WIN / 64];  // window scan: ready prefix, unassigned count
     u32 ntodo, t, nact, done, i, nact_eval;
+    u32 nxt;  // the sub-batch's next row for a free wave (rows t .. t + 15 go to waves 0 .. 15)
     u64 nexact, ntotal;
     u64 tr_begin, tr_started;  // BSMR_DIAG & 2048 timeline (ClusterArgs::ctrace)
-    u64 tr_t0, tr_scan, tr_eval, tr_lead;
+    u64 tr_t0, tr_scan, tr_eval, tr_lead, tr_own, tr_ent;
     u32 tr_win, tr_idle, tr_sub;
 };
 
@@ -371,10 +374,10 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
 #pragma unroll
             for (u32 u = 0; u < 4; ++u) {
                 const u32 blk = ent[u] & 0xFFFFu;
-                // a padding or non-kept entry contributes min(x, 0) = 0
-                const float y = (ent[u] && kept_idx(blk, a.B, a.keptMask))
-                                    ? static_cast<float>(ent[u] >> 16) * incf
-                                    : 0.0f;
+                // a padding (count 0) or non-kept entry contributes min(x, 0) = 0; the kept test
+                // (a division by B per entry) only when some warp of the tree is dropped
+                const float yr = static_cast<float>(ent[u] >> 16) * incf;
+                const float y = (a.allKept || kept_idx(blk, a.B, a.keptMask)) ? yr : 0.0f;
                 const u32* rp = reps + blk * TS;
                 u32 rv[TS];
                 if constexpr (TS % 4 == 0) {
@@ -407,9 +410,10 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
         constexpr u32 NX = TS <= 6 ? 4 * (CL_PRE_CH - 1) : 0;
         u32 ent[NX > 0 ? NX : 1];
 #pragma unroll
-        for (u32 u = 0; u < NX; ++u) {
+        for (u32 u = 0; u < NX; ++u) {  // clamped loads, no branch per load
             const u32 e = l + 256 + 64 * u;
-            ent[u] = e < nb ? a.enc[b0 + e] : 0u;
+            const u32 v = a.enc[b0 + min(e, nb - 1)];
+            ent[u] = e < nb ? v : 0u;
         }
         chunk(pre[0], pre[1], pre[2], pre[3]);
 #pragma unroll
@@ -420,7 +424,8 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
 #pragma unroll
             for (u32 u = 0; u < 4; ++u) {
                 const u32 e = e0 + 64 * u;
-                x[u] = e < nb ? a.enc[b0 + e] : 0u;
+                const u32 v = a.enc[b0 + min(e, nb - 1)];
+                x[u] = e < nb ? v : 0u;
             }
             chunk(x[0], x[1], x[2], x[3]);
         }
@@ -433,9 +438,11 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
 __device__ __forceinline__ void load_chunk0(const ClusterArgs& a, uint4 m, u32 (&ent)[4]) {
     const u32 l = lane_id();
 #pragma unroll
-    for (u32 u = 0; u < 4; ++u) {
+    for (u32 u = 0; u < 4; ++u) {  // clamped (rows hold >= 1 entry; m.y = 0: no row, no load)
         const u32 e = l + 64 * u;
-        ent[u] = e < m.y ? a.enc[m.x + e] : 0u;
+        u32 v = 0;
+        if (m.y) v = a.enc[m.x + min(e, m.y - 1)];
+        ent[u] = e < m.y ? v : 0u;
     }
 }
 
@@ -452,7 +459,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
     if (tid == 0) {
         C.tr_begin = a.ctrace ? now_ticks() : 0ull;
         C.tr_started = 0;
-        C.tr_scan = C.tr_eval = C.tr_lead = 0;
+        C.tr_scan = C.tr_eval = C.tr_lead = C.tr_own = C.tr_ent = 0;
         C.tr_win = C.tr_idle = C.tr_sub = 0;
     }
     if (tid < CL_TMAX) {
@@ -662,6 +669,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
             if (l == 0) {
                 C.ntodo = n;
                 C.t = 0;
+                C.nxt = CL_WAVES;
                 C.i = i + total;
                 if (aborted) {
                     C.done = 1;
@@ -691,7 +699,13 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                     load_chunk0(a, m, pre);
                 }
                 while (j < tend) {
-                    const u32 jn = j + CL_WAVES;
+                    // the next row comes from the sub-batch's counter: rows go to whichever wave
+                    // is free, so a long row no longer holds a fixed three others behind it
+                    // (wave 0 spent 40 % of the evaluation phase waiting at the barrier on
+                    // reddit-like x1; profiles/r03j/cltrace)
+                    u32 jn = 0;
+                    if (l == 0) jn = atomicAdd(&C.nxt, 1u);
+                    jn = __builtin_amdgcn_readfirstlane(jn);
                     const u32 cur[4] = {pre[0], pre[1], pre[2], pre[3]};
                     const uint4 mc = m;
                     if (jn < tend) {  // the next row's first chunk in flight while this one runs
@@ -700,9 +714,11 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                     }
                     const u32 r = eval_row<TS>(a, reps, C, mc, cur, nact);
                     if (l == 0) C.res[j] = r;
+                    if (a.ctrace && tid == 0) C.tr_ent += mc.y;
                     j = jn;
                 }
             }
+            if (a.ctrace && tid == 0) C.tr_own += now_ticks() - C.tr_t0;  // wave 0's own rows
             __syncthreads();
             if (a.ctrace && tid == 0) {
                 const u64 tn = now_ticks();
@@ -779,6 +795,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
                 }
                 if (l == 0) {
                     C.t = j;
+                    C.nxt = j + CL_WAVES;
                     C.nexact += nex;
                     C.ntotal += ntot;
                 }
@@ -793,7 +810,7 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
         atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[2]), C.nexact);
         atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctrl[4]), C.ntotal);
         if (a.ctrace) {
-            unsigned long long* tr = a.ctrace + 12ull * ((kfirst - 1) / T);
+            unsigned long long* tr = a.ctrace + 16ull * ((kfirst - 1) / T);
             tr[0] = C.tr_begin;
             tr[1] = C.tr_started;
             tr[2] = now_ticks();
@@ -806,6 +823,10 @@ __global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
             tr[9] = C.tr_eval;
             tr[10] = C.tr_lead;
             tr[11] = C.nexact;
+            tr[12] = C.tr_own;
+            tr[13] = C.tr_ent;
+            tr[14] = 0;
+            tr[15] = 0;
         }
     }
 }
@@ -2025,6 +2046,7 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     ca.nbpr = nbpr;
     ca.B = B;
     ca.keptMask = keptMask;
+    ca.allKept = keptMask == (B / 32 >= 32 ? 0xFFFFFFFFu : (1u << (B / 32)) - 1u) ? 1u : 0u;
     ca.alpha = alpha;
     ca.exact_all = exact_all;
     ca.timeout_ticks = 100ull * 1000 * 1000 * 20;  // 20 s without progress
@@ -2047,8 +2069,8 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     BSMR_HIP(hipMemsetAsync(cmpScratch.data(), 0, static_cast<size_t>(tilesMax) * nbpr * sizeof(u32), s));
     ca.cmpScratch = cmpScratch.data();
     ca.ctrace = nullptr;
-    if (diag & 2048) {  // clustering timeline (tools/cluster_trace.py): 12 u64 per tile
-        BSMR_CHECK(prepare_trace((static_cast<size_t>(M) / T + 2) * 3, s));
+    if (diag & 2048) {  // clustering timeline (tools/cluster_trace.py): 16 u64 per tile
+        BSMR_CHECK(prepare_trace((static_cast<size_t>(M) / T + 2) * 4, s));
         ca.ctrace = trace.data();
     }
     u32 c0 = 1;
