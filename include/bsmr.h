@@ -22,10 +22,11 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 6  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 7  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
-                              the plan options (no environment reads in the library) */
+                              the plan options (no environment reads in the library);
+                              7: bsmr_tuning.out_packed */
 
 typedef enum {
     BSMR_OK = 0,
@@ -122,6 +123,9 @@ typedef struct {
                                   and sparse-row patterns with fewer row blocks than slots sized
                                   to one block per slot; 0 = entry-even cuts, fewest-items deal,
                                   LDS-budget blocks; -1 = 1 */
+    int32_t out_packed;        /* BSMR_OUT_PACKED: unstaged row-block layouts carry each entry's CSR
+                                  position in its metadata word (one 4-byte load per entry instead
+                                  of two), 0 never, else whenever nnz <= 2^22; -1 = auto */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

@@ -46,7 +46,7 @@ class Tuning(C.Structure):
                 ("dense_ks", C.c_int32), ("dense_ns", C.c_int32), ("out_staged", C.c_int32),
                 ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32), ("seg_items", C.c_int32),
                 ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
-                ("item_sched", C.c_int32)]
+                ("item_sched", C.c_int32), ("out_packed", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -117,7 +117,7 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 6  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 7  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -234,7 +234,7 @@ def tuning_from_env(env=None):
         v = env.get(TUNING_ENV[f])
         if v is None:
             continue
-        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched"):  # tri-state: "0" never, "1" always, else auto
+        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
         elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap"):
             out[f] = float(v)

@@ -35,6 +35,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->late_b = -1;
     t->item_cap = -1.0f;
     t->item_sched = -1;
+    t->out_packed = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -81,6 +82,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     geti("BSMR_LATE_B", t->late_b);
     getf("BSMR_ITEM_CAP", t->item_cap);
     get3("BSMR_ITEM_SCHED", t->item_sched);
+    get3("BSMR_OUT_PACKED", t->out_packed);
     return n;
 }
 
@@ -127,6 +129,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->dense_ks >= 0) p.dense_ks = t->dense_ks;
         if (t->dense_ns >= 0) p.dense_ns = t->dense_ns;
         if (t->out_staged >= 0) p.out_staged = t->out_staged ? 1 : 0;
+        if (t->out_packed >= 0) p.out_packed = t->out_packed ? 1 : 0;
         if (t->stage_nt >= 0) p.stage_nt = t->stage_nt ? 1 : 0;
         if (t->seg_items >= 0) p.seg_items = t->seg_items;
         if (t->rb_rows > 0) p.rb_rows_force = t->rb_rows;

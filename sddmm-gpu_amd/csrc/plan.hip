@@ -1224,6 +1224,13 @@ __global__ void k_rb_gather_csr(const u32* __restrict__ order, const u32* __rest
 
 inline u32 grid_for(u64 n, u32 b) { return static_cast<u32>((n + b - 1) / b); }
 
+// packed output: metadata word = local row << 22 | CSR position (the column bits are only read
+// on the host, to cut the pieces, before this)
+__global__ void k_pack_out(u32* __restrict__ meta, const u32* __restrict__ out, u32 n) {
+    const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) meta[e] = (meta[e] & ~0x3FFFFFu) | out[e];
+}
+
 // staged output: item i's entries [ea, ea + E) sorted by CSR position (keys = positions, vals =
 // index inside the item): slot t of the sorted order -> the entry's metadata low bits, and the
 // position into sortedPos[ea + t]
@@ -1920,6 +1927,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     L.nPieces = static_cast<u32>(pieces.size());
     L.outLds = 0;
     L.outCap = 0;
+    L.outPacked = false;
     L.sortedPos.release();
     L.itemEnt.release();
     if (staged && n) {
@@ -1960,6 +1968,13 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         L.out.release();
         L.outLds = static_cast<u32>(lds);
         L.outCap = outCap;
+    } else if (n && out_packed != 0 && nnz <= (1u << 22)) {
+        hipLaunchKernelGGL(k_pack_out, dim3((n + 255) / 256), dim3(256), 0, s, L.meta.data(),
+                           L.out.data(), n);
+        BSMR_HIP(hipGetLastError());
+        BSMR_HIP(hipStreamSynchronize(s));
+        L.out.release();
+        L.outPacked = true;
     }
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
     BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));

@@ -69,6 +69,9 @@ struct Plan {
     // 1.394 -> 1.305 ms; C2 nips-like (3 MB, P stays in L2 and its scattered stores merge there)
     // 11.86 -> 12.60 us, so it stays on one store per entry
     int out_staged = -1;
+    // BSMR_OUT_PACKED: unstaged row-block layouts carry the CSR position in the metadata word
+    // (0 never, else whenever nnz <= 2^22)
+    int out_packed = -1;
     // A staging with the nt cache policy (BSMR_STAGE_NT: 0 never, 1 always, else auto = staged
     // output layouts when stage_nt_auto)
     int stage_nt = -1;
@@ -156,6 +159,9 @@ struct Plan {
         // number of entries} of item i; entries of an item never exceed the LDS tail past the
         // A image (outCap floats)
         u32 outLds = 0, outCap = 0;
+        // packed output (unstaged layouts of plans with nnz <= 2^22): the entry metadata's low 22
+        // bits hold the CSR position itself, so an entry costs one 4-byte metadata load (no out)
+        bool outPacked = false;
         DevBuf<u32> sortedPos;
         DevBuf<uint2> itemEnt;
         DevBuf<uint4> items;

@@ -416,6 +416,7 @@ struct RbArgs {
     // in LDS; the entry metadata's low bits are then the slot, and the workgroup writes the slots
     // to P[sortedPos[itemEnt.x + t]] at the end
     u32 outLds;
+    u32 outPacked;  // 1: no out array, the metadata's low 22 bits are the CSR position
     u32 stageNt;  // 1: stage the A rows with the nt policy (Plan::stage_nt)
     u32 lateB;    // 1: phase-0 B columns / metadata loaded after the staging barrier (late_b)
     const u32* sortedPos;
@@ -627,7 +628,7 @@ __device__ __forceinline__ void load_piece_body(const RbArgs& a, const u32 sub,
         // staged output: the slot is the metadata's low bits, taken where the result is stored
         // (deriving it here made the prologue wait for this load, and so for the B column
         // before it, ahead of the staging)
-        pc.mo[k] = !a.outLds && e < pc.len ? a.out[pc.first + e] : 0u;
+        pc.mo[k] = !a.outLds && !a.outPacked && e < pc.len ? a.out[pc.first + e] : 0u;
     }
 }
 
@@ -706,7 +707,7 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
                 *reinterpret_cast<float*>(const_cast<char*>(As) + a.outLds +
                                           4 * (pc.mm[k] & 0x3FFFFFu)) = res;
             else
-                a.P[pc.mo[k]] = res;
+                a.P[a.outPacked ? pc.mm[k] & 0x3FFFFFu : pc.mo[k]] = res;
         }
     }
 }
@@ -1032,6 +1033,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.meta = L.meta.data();
     a.out = L.out.data();
     a.outLds = (mode & 2) ? L.outLds : 0u;  // (dense-only profiling launches write no slots)
+    a.outPacked = L.outPacked ? 1u : 0u;
     a.stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
     a.lateB = p.late_b != 0;
     a.sortedPos = L.sortedPos.data();
