@@ -9,7 +9,7 @@ split built here:
    rows, so rank 0 builds the plan (``bsmr_plan_create``) and broadcasts its row stage (the
    ``bsmr_row_stage`` header and the reordered rows, u32 on the device) over RCCL. The other
    ranks rebuild the column stage from it (``bsmr_plan_import_rows``): clustering is most of the
-   plan time (reddit_like x1 on MI355X: 14.2 s of a 14.5 s plan), the column stage
+   plan time (reddit_like x1 on MI355X: 11.0 s of a 13 s plan), the column stage
    a deterministic O(nnz) pass (0.18 s) that is cheaper to recompute than to ship (its arrays are
    ~12 B per entry, ~2.8 GB for reddit_like x1, against 0.9 MB of row stage).
 2. **Panel cut.** Every rank holds the same global plan, so every rank computes the same cost-model

@@ -89,6 +89,7 @@ def main():
     xcc = (runs[-1][: nitems * wpg].reshape(nitems, wpg, 4)[:, 0, 3] >> np.uint64(60)).astype(np.int64) & 0xF
     np.savez(args.out + ".npz", rb=stat[:, 0], tiles=stat[:, 1], entries=stat[:, 2],
              pieces=stat[:, 3], start_us=start, dur_us=dur, xcc=xcc,
+             dur_all=np.stack([p[1] for p in per_item]), start_all=np.stack([p[0] for p in per_item]),
              meta=np.array([RB, NT, nitems, rowBytes, K, M, N, len(ci)], np.int64))
     work = stat[:, 2] > 0
     st = plan.stats()
