@@ -1436,8 +1436,16 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // 256 / 512: 379 -> 358 us and 896 -> 771 us against the 120 KiB staged image;
     // profiles/r03f/itemcal); 512-byte rows keep the tuned 120 KiB staged image (C4)
     const u32 stagedKb = !item_cost_cuts || rowBytes <= 512 ? rb_lds_kb_staged : rowBytes <= 1024 ? 80u : 160u;
-    const u32 ldsKb = stagedWanted && !rb_lds_user ? stagedKb : rb_lds_kb;
-    const u32 l2Kb = stagedWanted && !l2_range_user ? l2_range_kb_staged : l2_range_kb;
+    // 2 KiB rows (fp32 K = 512, fp16/bf16 K = 1024) take the whole-LDS image and 8 MiB column
+    // ranges whatever P's size: an item's A image is 80 rows x 2 KiB, and fewer, wider ranges
+    // restage it less (mycielskian14 / 15 / 16 K = 512: 100 -> 87, 253 -> 238, 735 -> 716 us;
+    // 1 KiB rows lose with 8 MiB ranges: mycielskian16 K = 256 358 -> 468 us; profiles/r03u).
+    // Sparse rows (< 64 stored entries per row) keep the small-row-block rule below (Trefethen
+    // K = 512: 48-row blocks 48.1 us, 80-row blocks 51.5 us; profiles/r03v)
+    const bool bigRows = item_cost_cuts && rowBytes >= 2048 && n0 >= 64ull * Rs;
+    const u32 ldsKb = (stagedWanted || bigRows) && !rb_lds_user ? stagedKb : rb_lds_kb;
+    const u32 l2Kb = l2_range_user ? l2_range_kb
+                                   : bigRows ? 8192u : stagedWanted ? l2_range_kb_staged : l2_range_kb;
     u32 RBr = rowblock_rows(rowBytes, ldsKb, Rs);
     {
         // sparse rows (< 64 stored entries per row: banded / FEM patterns) keep their row blocks
