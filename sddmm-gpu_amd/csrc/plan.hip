@@ -1444,8 +1444,12 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // K = 512: 48-row blocks 48.1 us, 80-row blocks 51.5 us; profiles/r03v)
     const bool bigRows = item_cost_cuts && rowBytes >= 2048 && n0 >= 64ull * Rs;
     const u32 ldsKb = (stagedWanted || bigRows) && !rb_lds_user ? stagedKb : rb_lds_kb;
+    // staged 512-byte rows (C4 reddit-like x1 fp32 K = 128): 8 MiB ranges too, half the A
+    // restaging for a B range twice the L2 (4.01 -> 3.89 ms over three alternating runs,
+    // profiles/r03y; C3 fp16 K = 256 neutral)
     const u32 l2Kb = l2_range_user ? l2_range_kb
-                                   : bigRows ? 8192u : stagedWanted ? l2_range_kb_staged : l2_range_kb;
+                     : bigRows || (stagedWanted && item_cost_cuts && rowBytes == 512) ? 8192u
+                     : stagedWanted ? l2_range_kb_staged : l2_range_kb;
     u32 RBr = rowblock_rows(rowBytes, ldsKb, Rs);
     {
         // sparse rows (< 64 stored entries per row: banded / FEM patterns) keep their row blocks
