@@ -122,7 +122,8 @@ typedef struct {
                                   scheduled heaviest first onto the XCD where they start earliest,
                                   and sparse-row patterns with fewer row blocks than slots sized
                                   to one block per slot; 0 = entry-even cuts, fewest-items deal,
-                                  LDS-budget blocks; -1 = 1 */
+                                  LDS-budget blocks (the item_cap still applies: with item_cap
+                                  = 0 as well this is the round-2 layout); -1 = 1 */
     int32_t out_packed;        /* BSMR_OUT_PACKED: unstaged row-block layouts carry each entry's CSR
                                   position in its metadata word (one 4-byte load per entry instead
                                   of two), 0 never, else whenever nnz <= 2^22; -1 = auto */
@@ -282,7 +283,9 @@ int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtype, int rank
 /* Measured-cost rebalancing of the row-block cut: prev_cuts[world+1] are the panel cuts the ranks
  * ran (bsmr_plan_shard_dtype's, or an earlier rebalance) and shard_ms[world] the time each shard
  * took; every row block's model cost is scaled by its shard's measured / predicted ratio and the
- * plan is cut again (cuts[world+1], row-block boundaries). Deterministic in its inputs, so every
+ * plan is cut again (cuts[world+1], row-block boundaries). A shard whose time is 0, NaN or inf
+ * counts as unmeasured: its row blocks keep their model cost (scaled by the measured shards' mean
+ * factor). Deterministic in its inputs, so every
  * rank derives the same cuts from the same gathered times. Row-block launches of reordered
  * plans only, else BSMR_ERR_UNSUPPORTED. */
 int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int dtype, int world,

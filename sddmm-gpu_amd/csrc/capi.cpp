@@ -534,6 +534,7 @@ extern "C" int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int 
     }
     // each row block's model cost scaled by its shard's measured / predicted time
     std::vector<double> scale(nRB, 1.0);
+    std::vector<char> measured(nRB, 0);
     for (int r = 0; r < world; ++r) {
         if (prev_cuts[r + 1] < prev_cuts[r] || (prev_cuts[r] % ppr && prev_cuts[r] != p.P)) {
             set_error("bsmr_plan_shard_rebalance: previous cuts are not row-block boundaries");
@@ -542,19 +543,25 @@ extern "C" int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int 
         const u32 b0 = prev_cuts[r] / ppr, b1 = std::min(nRB, (prev_cuts[r + 1] + ppr - 1) / ppr);
         double pred = 0.0;
         for (u32 b = b0; b < b1; ++b) pred += L->rbCost[b];
-        if (pred <= 0.0 || !(shard_ms[r] > 0.0f)) continue;
+        if (pred <= 0.0 || !(shard_ms[r] > 0.0f) || !std::isfinite(shard_ms[r])) continue;
         const double f = static_cast<double>(shard_ms[r]) / pred;
-        for (u32 b = b0; b < b1; ++b) scale[b] = f;
+        for (u32 b = b0; b < b1; ++b) {
+            scale[b] = f;
+            measured[b] = 1;
+        }
     }
-    // normalise the factors of measured shards to their mean, so unmeasured blocks keep weight 1
+    // normalise the factors of measured blocks to their mean; unmeasured blocks (a shard whose
+    // time is 0 / NaN / inf) take the mean factor, i.e. keep their model cost
     double fs = 0.0;
     u32 nf = 0;
     for (u32 b = 0; b < nRB; ++b)
-        if (scale[b] != 1.0) {
+        if (measured[b]) {
             fs += scale[b];
             ++nf;
         }
     const double norm = nf ? fs / nf : 1.0;
+    for (u32 b = 0; b < nRB; ++b)
+        if (!measured[b]) scale[b] = norm;
     std::vector<double> cum(nRB + 1ull, 0.0);
     for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b] * (scale[b] / norm);
     cut_row_blocks(cum, nRB, ppr, p.P, world, cuts);

@@ -1350,7 +1350,9 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q, double cap = 
         out[i] = std::max<u32>(1, static_cast<u32>(std::floor(ideal)));
         if (cap > 0) out[i] = std::max<u32>(out[i], static_cast<u32>(std::ceil(cost[i] / cap)));
         used += out[i];
-        frac.push_back({ideal - out[i], i});
+        // capped: rank by what is still missing; uncapped: by the fractional part (the round-2
+        // rule, so BSMR_ITEM_SCHED=0 BSMR_ITEM_CAP=0 reproduces the round-2 item lists)
+        frac.push_back({cap > 0 ? ideal - out[i] : ideal - std::floor(ideal), i});
     }
     std::stable_sort(frac.begin(), frac.end(),
                      [](const auto& a, const auto& b) { return a.first > b.first; });

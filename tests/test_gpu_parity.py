@@ -273,6 +273,43 @@ def test_rowblock_layout_variants(env, K, dtype):
         assert np.isfinite(Ps).all() and O.check_data(ref, Ps) == 0, name
 
 
+@functools.lru_cache(maxsize=None)
+def wide_case():
+    # N = 400 K: 512-byte B rows make 25.6 MB per XCD share, so the staged default of 8 MiB
+    # column ranges gives m = 4 ranges per XCD (the 4 MiB rule gave 7), with split row blocks
+    return synth.random_rows(2048, 400000, 400, seed=9, zipf=1.1)
+
+
+@pytest.mark.parametrize("env,K,dtype", [
+    ({"BSMR_OUT_STAGED": "1"}, 128, 0),                            # C4's default: 8 MiB ranges
+    ({"BSMR_OUT_STAGED": "1"}, 256, 1),                            # C3's row size, fp16
+    ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "8192"}, 128, 0),  # the same, set explicitly
+    ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "4096"}, 128, 0),  # the round-3 staged rule
+    ({}, 128, 0),                                                  # unstaged (P < 8 MiB)
+])
+def test_staged_default_column_ranges_wide(env, K, dtype):
+    """The staged 512-byte-row default (8 MiB XCD column ranges, plan.hip build_rowblock_layout)
+    on a pattern wide enough for several ranges per XCD: values equal the oracle's, and the
+    whole-plan launch splits row blocks by range (more items than row blocks)."""
+    M, N, rp, ci = wide_case()
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock",
+                tuning=tuning_from_env(env))
+    A = make_data(M * K)
+    B = make_data(N * K)
+    P = run_sddmm(plan, A, B, K, len(ci), dtype=dtype)
+    if dtype:
+        A, B = half_values(A, dtype), half_values(B, dtype)
+    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
+    assert np.isfinite(P).all()
+    assert O.check_data(ref, P) == 0
+    s = plan.stats()  # 512-byte rows: layout slot 2 (fp32 K = 128, half K = 256)
+    rb = s["rb_rows"][2]
+    assert rb > 0 and s["rb_items"][2] > (s["num_reordered_rows"] + rb - 1) // rb
+    shards = [plan.shard(K, r, 2, dtype) for r in range(2)]
+    Ps = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
+    assert np.isfinite(Ps).all() and O.check_data(ref, Ps) == 0
+
+
 def test_values_independent_of_layout_permutation():
     """Size-independent property: P of the same S is identical for every alpha/delta plan."""
     M, N, rp, ci = small_cases()["zipf"]

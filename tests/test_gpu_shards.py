@@ -240,5 +240,10 @@ def test_shard_rebalance_moves_cuts_toward_measured_balance():
     assert slow[1] <= cuts[1] and slow[-1] == P
     assert all(c % rb == 0 or c == P for c in slow)
     assert all(a <= b for a, b in zip(slow, slow[1:]))
+    # unmeasured shards (time 0 / NaN) keep their model cost: with the measured ones at equal
+    # time per model cost (real ms-scale values, far from 1.0), the cuts stay at the model cut
+    for ms in ([0.0012, 0.0, 0.0012, float("nan")], [0.0, 0.0012, float("inf"), 0.0012]):
+        kept = plan.shard_rebalance(K, world, cuts, ms)
+        assert all(abs(a - b) <= rb for a, b in zip(kept, cuts)), (ms, kept, cuts)
     with pytest.raises(Exception):
         plan.shard_rebalance(K, world, cuts[:-1] + [P - 1], [1.0] * world)

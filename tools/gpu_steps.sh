@@ -1,0 +1,70 @@
+#!/bin/bash
+# One gpurun pass made of named steps, each under its own time limit, stopping at the first
+# failure:   bash tools/gpu_steps.sh <tag> <step> [<step> ...]
+# Outputs go to gpurun_out/<tag>/ (steps.log records the order and timing).
+#   smoke                   __graft_entry__.smoke()
+#   tests                   the whole pytest -m gpu suite (-v, per-test timeout)
+#   tests:<expr>            pytest -m gpu -k <expr>
+#   bench:<cfg>             bench.py line of one config (C1 C2 C3 C4 C4x1 C5u C5b C2k32 C2k512)
+#   quick:<cfg>             the same without the CPU / vendor legs and PMC passes
+#   rocprof:<cfg>           rocprofv3 --kernel-trace --stats of that config's bench (every traced
+#                           launch a timed step)
+#   strong:<scale>          bench's multi-GPU path on one GPU under torchrun (RCCL, world 1) with
+#                           the strong_C4 block at that reddit-like scale
+#   ss                      tools/suitesparse_compare.py (five rebuilt SuiteSparse matrices)
+#   hybrid                  tools/hybrid_table.py (-t 1 logs of the five matrices + analyzer table)
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+log() { echo "[$(date +%T)] $*" >> "$OUT/steps.log"; }
+
+cfg_args() {
+    case "$1" in
+        C1) echo "--config C1" ;;
+        C2) echo "--config C2" ;;
+        C2k32) echo "--config C2 --K 32" ;;
+        C2k512) echo "--config C2 --K 512" ;;
+        C3) echo "--config C3 --steps 50 --warmup 5" ;;
+        C4) echo "--config C4 --steps 20 --warmup 3" ;;
+        C4x1) echo "--config C4 --scale 1.0 --steps 20 --warmup 3 --cold-steps 0" ;;
+        C5u) echo "--config C5 --mask uniform --steps 100 --warmup 10" ;;
+        C5b) echo "--config C5 --mask block --steps 100 --warmup 10" ;;
+        *) echo "unknown config $1" >&2; return 1 ;;
+    esac
+}
+QUICK="--no-cpu-baseline --no-vendor --pmc off"
+
+run_step() {
+    local s=$1 name=${1%%:*} arg=${1#*:}
+    local f=${s//[:\/ ]/_}
+    log "start $s"
+    case "$name" in
+        smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+        tests)
+            if [ "$arg" = "$s" ]; then
+                timeout -k 10 1500 python3 -u -m pytest tests -x -v -m gpu --timeout 600 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+            else
+                timeout -k 10 900 python3 -u -m pytest tests -x -v -m gpu -k "$arg" --timeout 600 --timeout-method thread > "$OUT/$f.log" 2>&1
+            fi ;;
+        bench) timeout -k 10 900 python3 bench.py $(cfg_args "$arg") > "$OUT/bench_$arg.json" 2> "$OUT/bench_$arg.err" ;;
+        quick) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") $QUICK > "$OUT/quick_$arg.json" 2> "$OUT/quick_$arg.err" ;;
+        rocprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$arg" -o run -- \
+                     python3 bench.py $(cfg_args "$arg") $QUICK --no-split > "$OUT/rocprof_$arg.json" 2> "$OUT/rocprof_$arg.err" ;;
+        strong) timeout -k 10 1000 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                     --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --force-sharded \
+                     --strong on --strong-scale "$arg" --no-vendor --pmc off > "$OUT/strong_$arg.json" 2> "$OUT/strong_$arg.err" ;;
+        ss) timeout -k 10 1000 python3 -u tools/suitesparse_compare.py --out "$OUT/ss" > "$OUT/ss.log" 2>&1 ;;
+        hybrid) timeout -k 10 1100 python3 -u tools/hybrid_table.py --out "$OUT/hybrid" > "$OUT/hybrid.log" 2>&1 ;;
+        *) echo "unknown step $s" >&2; return 2 ;;
+    esac
+    local rc=$?
+    log "end $s rc=$rc"
+    return $rc
+}
+
+for s in "$@"; do
+    run_step "$s" || { rc=$?; log "stopped at $s rc=$rc"; exit $rc; }
+done
+log "done"
