@@ -888,19 +888,36 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             // load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5: 1.135 ->
             // 1.082 ms). Issuing the first batch before the barrier measured slower (1.109 ms)
             constexpr u32 U = 8;
-            for (u32 t0 = tid; t0 < ie.y; t0 += U * NT) {
-                u32 pos[U];
+            auto pass = [&](auto nt_tag) {
+                constexpr bool NTS = decltype(nt_tag)::value;
+                for (u32 t0 = tid; t0 < ie.y; t0 += U * NT) {
+                    u32 pos[U];
 #pragma unroll
-                for (u32 k = 0; k < U; ++k) {
-                    const u32 t = t0 + k * NT;
-                    pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
-                }
+                    for (u32 k = 0; k < U; ++k) {
+                        const u32 t = t0 + k * NT;
+                        if constexpr (NTS)
+                            pos[k] = t < ie.y ? __builtin_nontemporal_load(a.sortedPos + ie.x + t) : 0u;
+                        else
+                            pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
+                    }
 #pragma unroll
-                for (u32 k = 0; k < U; ++k) {
-                    const u32 t = t0 + k * NT;
-                    if (t < ie.y) a.P[pos[k]] = res[t];
+                    for (u32 k = 0; k < U; ++k) {
+                        const u32 t = t0 + k * NT;
+                        if (t < ie.y) {
+                            if constexpr (NTS)
+                                __builtin_nontemporal_store(res[t], a.P + pos[k]);
+                            else
+                                a.P[pos[k]] = res[t];
+                        }
+                    }
                 }
-            }
+            };
+            // BSMR_DIAG & 4096 (experiment): the position loads and P stores with the
+            // nontemporal policy, so the store pass streams past the L2 lines of B and A
+            if (a.diag & 4096)
+                pass(std::true_type{});
+            else
+                pass(std::false_type{});
         }
     }
     trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);

@@ -183,6 +183,8 @@ def test_bench_sharded_two_ranks_one_gpu(extra):
         assert sum(sh["panels"]) == out["config"]["num_row_panels"]
         assert min(sh["panels"]) > 0
     assert out["scaling"] == ("weak" if "C2" in extra else "strong")
+    # the weak-scaling value says what it is: independent per-rank replicas of C2
+    assert ("independent replicas" in out.get("scaling_detail", "")) == ("C2" in extra)
     if "--strong-scale" in extra:  # the default N > 1 line carries the north_star reddit split
         sc = out["strong_C4"]
         for split in ("global", "local"):

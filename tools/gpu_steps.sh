@@ -13,6 +13,8 @@
 #                           the strong_C4 block at that reddit-like scale
 #   ss                      tools/suitesparse_compare.py (five rebuilt SuiteSparse matrices)
 #   hybrid                  tools/hybrid_table.py (-t 1 logs of the five matrices + analyzer table)
+#   ab:VAR:v1,v2:cfg1,cfg2  tools/ab_env.sh: alternating A/B of one BSMR_* knob (VAR without the
+#                           prefix may list several, joined by '+') on ab_env.sh's configs
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -56,7 +58,9 @@ run_step() {
                      --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --force-sharded \
                      --strong on --strong-scale "$arg" --no-vendor --pmc off > "$OUT/strong_$arg.json" 2> "$OUT/strong_$arg.err" ;;
         ss) timeout -k 10 1000 python3 -u tools/suitesparse_compare.py --out "$OUT/ss" > "$OUT/ss.log" 2>&1 ;;
-        hybrid) timeout -k 10 1100 python3 -u tools/hybrid_table.py --out "$OUT/hybrid" > "$OUT/hybrid.log" 2>&1 ;;
+        hybrid) timeout -k 10 1100 python3 -u tools/hybrid_table.py --run --out "$OUT/hybrid" > "$OUT/hybrid.log" 2>&1 ;;
+        ab) IFS=: read -r _ var vals cfgs <<< "$s"
+            timeout -k 10 1100 bash tools/ab_env.sh "$TAG/ab_${var//+/_}" "BSMR_${var//+/,BSMR_}" "${vals//,/ }" "${cfgs//,/ }" > "$OUT/$f.log" 2>&1 ;;
         *) echo "unknown step $s" >&2; return 2 ;;
     esac
     local rc=$?
