@@ -2,7 +2,7 @@
 
 The fixtures are the 140 log files the drop-in binary wrote in test mode on MI355X
 (`BSMR-sddmm -f Trefethen_20000.mtx -t 1 -l dir/`, sddmm.cu:62-118: 5 alpha x 7 delta x
-K in {32, 64, 128, 256}; tools/gpu_r03a.sh). The reference's scripts/analyze_results.cpp is compiled
+K in {32, 64, 128, 256}; tools/hybrid_table.py --run). The reference's scripts/analyze_results.cpp is compiled
 here from its own source with g++ (it is standalone C++, analyze_results.cpp:1-14) and run per K as
 scripts/plot_fig_5.sh does; it must accept the log set (SettingInformation::initInformation,
 analyze_results.cpp:122-160, rejects logs whose settings differ) and its results_<K>.csv must carry
