@@ -229,7 +229,8 @@ def mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles):
 
 def forced_mfma_split(args, pattern, K, dtype, dA, dB, dev, stream, P_ref, flops):
     """The config's dense-tile vs residual split when the default layout keeps no MFMA tile: the
-    same pattern planned with every BSMR tile kept on the matrix cores (tile_min = 0), its fused
+    same pattern planned with every BSMR tile kept on the matrix cores (tile_min = 0, reordered
+    row blocks), its fused
     launch timed like the line's steps, then its dense-tile-only and residual-only launches
     (bsmr_sddmm_profile) — the reference times its two streams separately
     (sddmmKernel.cu:2555-2659). P is checked against the line's P."""
@@ -240,6 +241,7 @@ def forced_mfma_split(args, pattern, K, dtype, dA, dB, dev, stream, P_ref, flops
     M, N, rp, ci = pattern
     tun = dict(args.tuning or {})
     tun["tile_min_f32" if dtype == F32 else "tile_min_half"] = 0
+    tun["orig_rows"] = 0  # original-order row blocks carry no tiles (every entry residual)
     plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=args.delta, device=dev.index,
                 layout=args.layout, tuning=tun)
     dP = torch.zeros(len(ci), dtype=torch.float32, device=dev)
@@ -703,7 +705,8 @@ def main_single(args):
     if kern.startswith("k_sddmm_rb"):
         out["bounds"] = rowblock_bounds(st_after, rby, ms_per_step)
     out["mfma"] = mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles)
-    if no_tiles and not args.no_split and st["num_dense_tiles"] > 0 and nnz <= 20_000_000:
+    if (no_tiles and not dtiles and not args.no_split and st["num_dense_tiles"] > 0
+            and nnz <= 20_000_000):
         out["mfma"]["forced_tiles_split"] = forced_mfma_split(
             args, (M, N, rp, ci), K, dtype, dA, dB, dev, stream, P_gpu, flops_rank)
     if cold_ms is not None:

@@ -1942,8 +1942,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     L.outLds = 0;
     L.outCap = 0;
     L.outPacked = false;
+    L.outRuns = false;
     L.sortedPos.release();
     L.itemEnt.release();
+    L.runs.release();
+    L.itemRuns.release();
     if (staged && n) {
         // slots: per item, its entries sorted by CSR position (segmented radix sort on the device)
         BSMR_CHECK(L.itemEnt.upload(ient.data(), ient.size(), s));
@@ -1982,6 +1985,41 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         L.out.release();
         L.outLds = static_cast<u32>(lds);
         L.outCap = outCap;
+        // run table (BSMR_DIAG & 8192: keep the per-result positions): consecutive CSR positions
+        // of an item's sorted slots form one run; used when no item has more runs than the
+        // workgroup has lanes (one descriptor per lane, loaded in the prologue)
+        L.outRuns = false;
+        L.runs.release();
+        L.itemRuns.release();
+        if (!(diag & 8192) && outCap < 65536) {
+            std::vector<u32> hpos(n);
+            BSMR_HIP(hipMemcpyAsync(hpos.data(), L.sortedPos.data(), n * sizeof(u32),
+                                    hipMemcpyDeviceToHost, s));
+            BSMR_HIP(hipStreamSynchronize(s));
+            std::vector<uint2> hr;
+            hr.reserve(n / 16 + ient.size());
+            std::vector<uint2> hir(ient.size(), make_uint2(0, 0));
+            bool fits = true;
+            for (size_t i = 0; i < ient.size() && fits; ++i) {
+                const u32 e0 = ient[i].x, len = ient[i].y;
+                const size_t r0 = hr.size();
+                for (u32 t = 0; t < len;) {
+                    u32 u = t + 1;
+                    while (u < len && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
+                    hr.push_back(make_uint2(hpos[e0 + t], t | ((u - t) << 16)));
+                    t = u;
+                }
+                hir[i] = make_uint2(static_cast<u32>(r0), static_cast<u32>(hr.size() - r0));
+                fits = hir[i].y <= NT;
+            }
+            if (fits) {
+                BSMR_CHECK(L.runs.upload(hr.data(), std::max<size_t>(hr.size(), 1), s));
+                BSMR_CHECK(L.itemRuns.upload(hir.data(), std::max<size_t>(hir.size(), 1), s));
+                BSMR_HIP(hipStreamSynchronize(s));
+                L.sortedPos.release();
+                L.outRuns = true;
+            }
+        }
     } else if (n && out_packed != 0 && nnz <= (1u << 22)) {
         hipLaunchKernelGGL(k_pack_out, dim3((n + 255) / 256), dim3(256), 0, s, L.meta.data(),
                            L.out.data(), n);

@@ -164,6 +164,13 @@ struct Plan {
         bool outPacked = false;
         DevBuf<u32> sortedPos;
         DevBuf<uint2> itemEnt;
+        // run table (staged output, outRuns): the item's slots in CSR order cut into runs of
+        // consecutive positions (one per row it touches when rows are column-sorted): runs[j] =
+        // {first position, first slot | length << 16}, itemRuns[i] = {first run, number of runs}
+        // (<= NT, one per lane); the store pass then reads 8 bytes per run instead of a position
+        // per result, and sortedPos is released
+        bool outRuns = false;
+        DevBuf<uint2> runs, itemRuns;
         DevBuf<uint4> items;
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}

@@ -421,6 +421,10 @@ struct RbArgs {
     u32 lateB;    // 1: phase-0 B columns / metadata loaded after the staging barrier (late_b)
     const u32* sortedPos;
     const uint2* itemEnt;
+    // staged output by runs (RowBlockLayout::outRuns; else null): {position, slot | len << 16}
+    // per run of consecutive CSR positions, {first run, runs} per item
+    const uint2* runs;
+    const uint2* itemRuns;
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
@@ -792,6 +796,16 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     pc.len = 0;
     if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
     if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
+    // staged output by runs: this lane's run descriptor (run w + NW * lane of the item), loaded
+    // now so the store pass at the end waits for nothing but the LDS slots
+    uint2 myrun = make_uint2(0u, 0u), irun = make_uint2(0u, 0u);
+    if (a.runs && a.outLds) {
+        irun = a.itemRuns[blockIdx.x];
+        irun.x = __builtin_amdgcn_readfirstlane(irun.x);
+        irun.y = __builtin_amdgcn_readfirstlane(irun.y);
+        const u32 j = w + NW * lane;
+        if (j < irun.y) myrun = a.runs[irun.x + j];
+    }
     // AUX: the LDS-DMA cache policy (0 default; 2 = nt, stream the A rows past the XCD's L2 so the
     // B columns of the item's column range stay resident: large staged-output layouts, where an
     // item's row block is not staged again on that XCD until the next range)
@@ -912,12 +926,23 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                     }
                 }
             };
-            // BSMR_DIAG & 4096 (experiment): the position loads and P stores with the
-            // nontemporal policy, so the store pass streams past the L2 lines of B and A
-            if (a.diag & 4096)
+            if (a.runs) {
+                // wave w writes runs w, w + NW, ...: one contiguous store of up to 64 results
+                // per run and step (a row's results in this item, when rows are column-sorted)
+                const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
+                for (u32 i = 0; i < nr; ++i) {
+                    const u32 pos = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), i));
+                    const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), i));
+                    const u32 s0 = sl & 0xFFFFu, len = sl >> 16;
+                    for (u32 k = lane; k < len; k += 64) a.P[pos + k] = res[s0 + k];
+                }
+            } else if (a.diag & 4096) {
+                // BSMR_DIAG & 4096 (experiment): the position loads and P stores with the
+                // nontemporal policy, so the store pass streams past the L2 lines of B and A
                 pass(std::true_type{});
-            else
+            } else {
                 pass(std::false_type{});
+            }
         }
     }
     trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
@@ -1055,6 +1080,8 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.lateB = p.late_b != 0;
     a.sortedPos = L.sortedPos.data();
     a.itemEnt = L.itemEnt.data();
+    a.runs = L.outRuns ? L.runs.data() : nullptr;
+    a.itemRuns = L.outRuns ? L.itemRuns.data() : nullptr;
     a.tilePanel = p.denseItems.data();
     a.tileIds = L.tileIds.data();
     a.denseCols = p.denseCols.data();
