@@ -797,15 +797,18 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
     if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
     // staged output by runs: this lane's run descriptor (run w + NW * lane of the item), loaded
-    // now so the store pass at the end waits for nothing but the LDS slots
+    // in the item's last piece phase, where the next-phase prefetch registers are free, so the
+    // store pass waits for nothing but the LDS slots
     uint2 myrun = make_uint2(0u, 0u), irun = make_uint2(0u, 0u);
-    if (a.runs && a.outLds) {
-        irun = a.itemRuns[blockIdx.x];
-        irun.x = __builtin_amdgcn_readfirstlane(irun.x);
-        irun.y = __builtin_amdgcn_readfirstlane(irun.y);
-        const u32 j = w + NW * lane;
-        if (j < irun.y) myrun = a.runs[irun.x + j];
-    }
+    auto load_runs = [&]() {
+        if (a.runs && a.outLds) {
+            irun = a.itemRuns[blockIdx.x];
+            irun.x = __builtin_amdgcn_readfirstlane(irun.x);
+            irun.y = __builtin_amdgcn_readfirstlane(irun.y);
+            const u32 j = w + NW * lane;
+            if (j < irun.y) myrun = a.runs[irun.x + j];
+        }
+    };
     // AUX: the LDS-DMA cache policy (0 default; 2 = nt, stream the A rows past the XCD's L2 so the
     // B columns of the item's column range stay resident: large staged-output layouts, where an
     // item's row block is not staged again on that XCD until the next range)
@@ -880,13 +883,19 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         pn.len = 0;
         if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
     };
-    if (NG < np) fetch(1);
+    if (NG < np)
+        fetch(1);
+    else
+        load_runs();
     if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     for (u32 ph = 1; ph * NG < np; ++ph) {
         pc = pn;
 #pragma unroll
         for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
-        if ((ph + 1) * NG < np) fetch(ph + 1);
+        if ((ph + 1) * NG < np)
+            fetch(ph + 1);
+        else
+            load_runs();
         if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     }
     for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
@@ -902,46 +911,46 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             // load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5: 1.135 ->
             // 1.082 ms). Issuing the first batch before the barrier measured slower (1.109 ms)
             constexpr u32 U = 8;
-            auto pass = [&](auto nt_tag) {
-                constexpr bool NTS = decltype(nt_tag)::value;
+            auto pass = [&]() {
                 for (u32 t0 = tid; t0 < ie.y; t0 += U * NT) {
                     u32 pos[U];
 #pragma unroll
                     for (u32 k = 0; k < U; ++k) {
                         const u32 t = t0 + k * NT;
-                        if constexpr (NTS)
-                            pos[k] = t < ie.y ? __builtin_nontemporal_load(a.sortedPos + ie.x + t) : 0u;
-                        else
-                            pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
+                        pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
                     }
 #pragma unroll
                     for (u32 k = 0; k < U; ++k) {
                         const u32 t = t0 + k * NT;
-                        if (t < ie.y) {
-                            if constexpr (NTS)
-                                __builtin_nontemporal_store(res[t], a.P + pos[k]);
-                            else
-                                a.P[pos[k]] = res[t];
-                        }
+                        if (t < ie.y) a.P[pos[k]] = res[t];
                     }
                 }
             };
             if (a.runs) {
                 // wave w writes runs w, w + NW, ...: one contiguous store of up to 64 results
                 // per run and step (a row's results in this item, when rows are column-sorted)
+                // four runs per step: their LDS reads in flight together
                 const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
-                for (u32 i = 0; i < nr; ++i) {
-                    const u32 pos = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), i));
-                    const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), i));
-                    const u32 s0 = sl & 0xFFFFu, len = sl >> 16;
-                    for (u32 k = lane; k < len; k += 64) a.P[pos + k] = res[s0 + k];
+                for (u32 i = 0; i < nr; i += 4) {
+                    u32 pos[4], s0[4], len[4];
+                    float v[4];
+#pragma unroll
+                    for (u32 u = 0; u < 4; ++u) {
+                        const u32 q = min(i + u, 63u);
+                        pos[u] = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), q));
+                        const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), q));
+                        s0[u] = sl & 0xFFFFu;
+                        len[u] = i + u < nr ? sl >> 16 : 0u;
+                        v[u] = lane < len[u] ? res[s0[u] + lane] : 0.0f;
+                    }
+#pragma unroll
+                    for (u32 u = 0; u < 4; ++u) {
+                        if (lane < len[u]) a.P[pos[u] + lane] = v[u];
+                        for (u32 k = lane + 64; k < len[u]; k += 64) a.P[pos[u] + k] = res[s0[u] + k];
+                    }
                 }
-            } else if (a.diag & 4096) {
-                // BSMR_DIAG & 4096 (experiment): the position loads and P stores with the
-                // nontemporal policy, so the store pass streams past the L2 lines of B and A
-                pass(std::true_type{});
             } else {
-                pass(std::false_type{});
+                pass();
             }
         }
     }
