@@ -1985,9 +1985,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         L.out.release();
         L.outLds = static_cast<u32>(lds);
         L.outCap = outCap;
-        // run table (BSMR_DIAG & 8192: keep the per-result positions): consecutive CSR positions
-        // of an item's sorted slots form one run; used when no item has more runs than the
-        // workgroup has lanes (one descriptor per lane, loaded in the prologue)
+        // run table (BSMR_DIAG & 8192: keep the per-result positions): up to 64 consecutive CSR
+        // positions of an item's sorted slots form one run; used when no item has more runs
+        // than the workgroup has lanes (one descriptor per lane, loaded in the last phase)
         L.outRuns = false;
         L.runs.release();
         L.itemRuns.release();
@@ -2004,8 +2004,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                 const u32 e0 = ient[i].x, len = ient[i].y;
                 const size_t r0 = hr.size();
                 for (u32 t = 0; t < len;) {
+                    // a run is one wave store: at most 64 consecutive positions (an unsplit
+                    // original-order item is one long run, which would leave all but one wave
+                    // idle in the store pass)
                     u32 u = t + 1;
-                    while (u < len && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
+                    while (u < len && u - t < 64 && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
                     hr.push_back(make_uint2(hpos[e0 + t], t | ((u - t) << 16)));
                     t = u;
                 }

@@ -421,7 +421,7 @@ struct RbArgs {
     u32 lateB;    // 1: phase-0 B columns / metadata loaded after the staging barrier (late_b)
     const u32* sortedPos;
     const uint2* itemEnt;
-    // staged output by runs (RowBlockLayout::outRuns; else null): {position, slot | len << 16}
+    // staged output by runs (RowBlockLayout::outRuns; else null): {position, slot | len << 16}, len <= 64
     // per run of consecutive CSR positions, {first run, runs} per item
     const uint2* runs;
     const uint2* itemRuns;
@@ -928,8 +928,8 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             };
             if (a.runs) {
                 // wave w writes runs w, w + NW, ...: one contiguous store of up to 64 results
-                // per run and step (a row's results in this item, when rows are column-sorted)
-                // four runs per step: their LDS reads in flight together
+                // per run (a row's results in this item, when rows are column-sorted), four
+                // runs per step with their LDS reads in flight together
                 const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
                 for (u32 i = 0; i < nr; i += 4) {
                     u32 pos[4], s0[4], len[4];
@@ -944,10 +944,8 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                         v[u] = lane < len[u] ? res[s0[u] + lane] : 0.0f;
                     }
 #pragma unroll
-                    for (u32 u = 0; u < 4; ++u) {
+                    for (u32 u = 0; u < 4; ++u)  // (runs are at most 64 long)
                         if (lane < len[u]) a.P[pos[u] + lane] = v[u];
-                        for (u32 k = lane + 64; k < len[u]; k += 64) a.P[pos[u] + k] = res[s0[u] + k];
-                    }
                 }
             } else {
                 pass();

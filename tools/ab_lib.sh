@@ -11,6 +11,7 @@ for c in $CFGS; do
         C2) ARGS="--workload nips_like --K 128 --dtype f32" ;;
         C3) ARGS="--workload cop20k_like --K 256 --dtype f16" ;;
         C4) ARGS="--workload reddit_like --scale 0.5 --K 128 --dtype f32" ;;
+        C4x1) ARGS="--workload reddit_like --scale 1.0 --K 128 --dtype f32" ;;
         C5u) ARGS="--workload dlmc_like --mask uniform --K 512 --dtype bf16" ;;
         C5b) ARGS="--workload dlmc_like --mask block --K 512 --dtype bf16" ;;
     esac
