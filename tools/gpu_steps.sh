@@ -4,7 +4,7 @@
 # Outputs go to gpurun_out/<tag>/ (steps.log records the order and timing).
 #   smoke                   __graft_entry__.smoke()
 #   tests                   the whole pytest -m gpu suite (-v, per-test timeout)
-#   tests:<expr>            pytest -m gpu -k <expr>
+#   tests:<a+b+...>         pytest -m gpu -k 'a or b or ...'
 #   bench:<cfg>             bench.py line of one config (C1 C2 C3 C4 C4x1 C5u C5b C2k32 C2k512)
 #   quick:<cfg>             the same without the CPU / vendor legs and PMC passes
 #   rocprof:<cfg>           rocprofv3 --kernel-trace --stats of that config's bench (every traced
@@ -49,7 +49,7 @@ run_step() {
             if [ "$arg" = "$s" ]; then
                 timeout -k 10 1500 python3 -u -m pytest tests -x -v -m gpu --timeout 600 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
             else
-                timeout -k 10 900 python3 -u -m pytest tests -x -v -m gpu -k "$arg" --timeout 600 --timeout-method thread > "$OUT/$f.log" 2>&1
+                timeout -k 10 900 python3 -u -m pytest tests -x -v -m gpu -k "${arg//+/ or }" --timeout 600 --timeout-method thread > "$OUT/${f//+/_}.log" 2>&1
             fi ;;
         bench) timeout -k 10 900 python3 bench.py $(cfg_args "$arg") > "$OUT/bench_$arg.json" 2> "$OUT/bench_$arg.err" ;;
         quick) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") $QUICK > "$OUT/quick_$arg.json" 2> "$OUT/quick_$arg.err" ;;
