@@ -1885,6 +1885,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     }
     size_t nmax = 0;
     for (const auto& l : lists) nmax = std::max(nmax, l.size());
+    // staged layouts: an even number of list positions, so the launch can pair them (k_sddmm_rb)
+    if (staged) nmax = (nmax + 1) & ~static_cast<size_t>(1);
     std::vector<uint4> items(nmax * XCD_BUCKETS, make_uint4(0, 0, 0, 0));
     std::vector<u32> ends(nmax * XCD_BUCKETS, 0);
     for (u32 x = 0; x < XCD_BUCKETS; ++x)

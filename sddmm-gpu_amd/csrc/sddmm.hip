@@ -425,6 +425,7 @@ struct RbArgs {
     // per run of consecutive CSR positions, {first run, runs} per item
     const uint2* runs;
     const uint2* itemRuns;
+    u32 pairs;  // 1: each workgroup runs list positions 2j and 2j + 1 of its XCD (see k_sddmm_rb)
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
@@ -716,36 +717,91 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
     }
 }
 
-template <int DT, int RBY, int NT>
-__global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char AsB[];
-    char* As = AsB;
-    if (blockIdx.y) {  // batch b (item -> XCD placement unchanged: nItems is a multiple of 8)
-        a.A += blockIdx.y * a.bA;
-        a.B += blockIdx.y * a.bB;
-        a.P += blockIdx.y * a.bP;
+constexpr u32 NO_ITEM = 0xFFFFFFFFu;
+// run values a wave holds in registers while the next item's staging is issued (pairs)
+constexpr u32 PAIR_RUNS_PER_WAVE = 16;
+
+// staging row indices of the row block starting at reordered position q0, one per lane (rows of
+// >= 256 bytes: lane l holds the row of block w + (l / NR) NW, rows l % NR of it)
+template <int RBY, int NT>
+__device__ __forceinline__ u32 rb_stage_rows(const RbArgs& a, const u32 q0, const u32 ws, const u32 lane) {
+    constexpr u32 NW = NT / 64, NCH = RBY / 16, NR = NCH >= 64 ? 1 : 64 / NCH;
+    constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
+    const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
+    return (i < MAXB && lr < a.RB && q < a.R) ? a.rows[q] : a.row0;
+}
+
+// the LDS-DMAs of one row block (rows of >= 256 bytes; rowv from rb_stage_rows): every wave
+// issues exactly MAXB 1 KiB blocks, back to back (see k_sddmm_rb)
+template <int DT, int RBY, int NT, int AUX>
+__device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const u32 rowv, const u32 ws,
+                                               const u32 lane) {
+    constexpr u32 NW = NT / 64, NCH = RBY / 16, NR = NCH >= 64 ? 1 : 64 / NCH;
+    constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
+    const u32 x0 = 64 * ws + lane;
+    const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
+#pragma unroll
+    for (u32 i = 0; i < MAXB; ++i) {
+        const u32 b = ws + i * NW;
+        u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
+#pragma unroll
+        for (u32 k = 1; k < NR; ++k) {
+            const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
+            src = lane / NCH == k ? rk : src;
+        }
+        const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(As + 1024 * b),
+                                         16, 0, AUX);
     }
+}
+
+// One row-block work item (see k_sddmm_rb). prestaged: the previous item of the workgroup's pair
+// already issued this item's staging. next (pairs, staged output by runs): the item that runs
+// next on this workgroup; its staging is issued in this item's store pass, right after the result
+// slots have been read into registers, so the next image lands while this item's stores drain.
+// Returns whether next's staging was issued (false: next is padding, or this item holds more
+// runs per wave than PAIR_RUNS_PER_WAVE and stored them the plain way).
+template <int DT, int RBY, int NT, bool PAIR>
+__device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx, const bool prestaged,
+                                        const u32 next) {
     using Geo = RowGeom<RBY>;
     constexpr u32 G = Geo::G, NC = Geo::NC;  // lanes per entry, chunks per lane
     constexpr u32 NW = NT / 64;               // waves per workgroup
     constexpr u32 NG = NT / G;                // residual row-groups
     constexpr u32 TC = DenseTileLds<DT, RBY>::CH;
-    const unsigned long long t0 = rtime(a.trace);
-    uint4 it = a.items[blockIdx.x];
+    // the pair kernel (PAIR): staged output by runs, no kept MFMA tiles, late B loads, default
+    // staging policy, no trace or ablations (launch_rb picks it only then): its two items fit
+    // the SGPR budget without those paths
+    const unsigned long long t0 = PAIR ? 0ull : rtime(a.trace);
+    uint4 it = a.items[idx];
     // all four fields in SGPRs before the padding test: the compiler otherwise loads .x (the row
     // block) in a second, dependent round trip after the test
     it.x = __builtin_amdgcn_readfirstlane(it.x);
     it.y = __builtin_amdgcn_readfirstlane(it.y);
     it.z = __builtin_amdgcn_readfirstlane(it.z);
     it.w = __builtin_amdgcn_readfirstlane(it.w);
-    const u32 pend = a.itemEnd[blockIdx.x];
-    if (it.y == it.z && it.w == pend) return;  // padding item (uniform across the workgroup)
+    const u32 pend = a.itemEnd[idx];
+    if (it.y == it.z && it.w == pend) return false;  // padding item (uniform across the workgroup)
+    // the next item of the pair: its row block (its staging rows are loaded in the last phase)
+    bool has_next = false;
+    u32 q0n = 0;
+    if (next != NO_ITEM) {
+        uint4 nt = a.items[next];
+        nt.x = __builtin_amdgcn_readfirstlane(nt.x);
+        nt.y = __builtin_amdgcn_readfirstlane(nt.y);
+        nt.z = __builtin_amdgcn_readfirstlane(nt.z);
+        nt.w = __builtin_amdgcn_readfirstlane(nt.w);
+        const u32 nend = __builtin_amdgcn_readfirstlane(a.itemEnd[next]);
+        has_next = !(nt.y == nt.z && nt.w == nend);
+        q0n = a.qbase + nt.x * a.RB;
+    }
     const u32 q0 = a.qbase + it.x * a.RB;
     const u32 tid = threadIdx.x, w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
     // every wave takes (at most) one dense tile and its row-groups one residual piece each per
     // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
     // staging loads so all of it is in flight together
-    const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
+    const u32 ntile = !PAIR && (a.mode & 1) ? it.z - it.y : 0u;
     const u32 np = (a.mode & 2) ? pend - it.w : 0u;
     const u32 gr = tid / G;
     u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
@@ -773,16 +829,17 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // trip overlaps the piece descriptor's, and the LDS-DMAs need not wait for the B columns
     u32 rowv = a.row0;
     u32 src[ROWV ? 1 : MAXB];
-    if constexpr (ROWV) {
-        const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
-        if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
-    } else {
-        // 128-byte rows: 8 rows per block, too many indices for one per lane; each lane loads
-        // the row of its own chunk for every block
+    if (!prestaged) {
+        if constexpr (ROWV) {
+            rowv = rb_stage_rows<RBY, NT>(a, q0, ws, lane);
+        } else {
+            // 128-byte rows: 8 rows per block, too many indices for one per lane; each lane
+            // loads the row of its own chunk for every block
 #pragma unroll
-        for (u32 i = 0; i < MAXB; ++i) {
-            const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
-            src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
+            for (u32 i = 0; i < MAXB; ++i) {
+                const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
+                src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
+            }
         }
     }
     // the loads the LDS-DMA issue waits for go first: row indices, the phase-0 piece descriptor
@@ -794,46 +851,37 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     const u32 tw = NW - 1 - w;
     Piece<RBY> pc;
     pc.len = 0;
-    if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
+    if constexpr (!PAIR)
+        if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
     if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
     // staged output by runs: this lane's run descriptor (run w + NW * lane of the item), loaded
-    // in the item's last piece phase, where the next-phase prefetch registers are free, so the
-    // store pass waits for nothing but the LDS slots
+    // when the wave's pieces are done, so the store pass waits (at most) for the slowest wave's
+    // descriptors; with a next item, its staging row indices are loaded there too
     uint2 myrun = make_uint2(0u, 0u), irun = make_uint2(0u, 0u);
+    u32 rown = a.row0;
     auto load_runs = [&]() {
         if (a.runs && a.outLds) {
-            irun = a.itemRuns[blockIdx.x];
+            irun = a.itemRuns[idx];
             irun.x = __builtin_amdgcn_readfirstlane(irun.x);
             irun.y = __builtin_amdgcn_readfirstlane(irun.y);
-            const u32 j = w + NW * lane;
-            if (j < irun.y) myrun = a.runs[irun.x + j];
+            const u32 jr = w + NW * lane;
+            if (jr < irun.y) myrun = a.runs[irun.x + jr];
         }
+        if constexpr (ROWV)
+            if (has_next) rown = rb_stage_rows<RBY, NT>(a, q0n, ws, lane);
     };
     // AUX: the LDS-DMA cache policy (0 default; 2 = nt, stream the A rows past the XCD's L2 so the
     // B columns of the item's column range stay resident: large staged-output layouts, where an
     // item's row block is not staged again on that XCD until the next range)
     auto stage = [&](auto aux_tag) {
         constexpr int AUX = decltype(aux_tag)::value;
-        // the source chunk of lane l is the same in every block of the wave: x % NCH and
-        // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
-        const u32 x0 = 64 * ws + lane;
-        const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
         if constexpr (ROWV) {
-#pragma unroll
-            for (u32 i = 0; i < MAXB; ++i) {
-                const u32 b = ws + i * NW;
-                u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
-#pragma unroll
-                for (u32 k = 1; k < NR; ++k) {
-                    const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
-                    src = lane / NCH == k ? rk : src;
-                }
-                const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                                 16, 0, AUX);
-            }
+            rb_stage_issue<DT, RBY, NT, AUX>(a, As, rowv, ws, lane);
         } else {
+            // the source chunk of lane l is the same in every block of the wave: x % NCH and
+            // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
+            const u32 x0 = 64 * ws + lane;
+            const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
 #pragma unroll
             for (u32 i = 0; i < MAXB; ++i) {
                 const u32 b = ws + i * NW;
@@ -844,14 +892,16 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             }
         }
     };
-    if (a.stageNt)
-        stage(std::integral_constant<int, 2>{});
-    else
-        stage(std::integral_constant<int, 0>{});
+    if (!prestaged) {
+        if (!PAIR && a.stageNt)
+            stage(std::integral_constant<int, 2>{});
+        else
+            stage(std::integral_constant<int, 0>{});
+    }
     // the phase-0 B columns and entry metadata: issued right behind the LDS-DMAs (so the
     // barrier's wait covers them too), or with lateB after the barrier (the barrier then waits
     // for the staging alone and the waves pay one load round trip before their first piece)
-    if (!a.lateB) {
+    if (!PAIR && !a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
         if (tw < ntile) dt.loadB(a, 0, tb);
     }
@@ -860,17 +910,19 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // not left to the compiler's wait insertion at the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (a.lateB) {
+    if (PAIR || a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
-        if (tw < ntile) dt.loadB(a, 0, tb);
+        if constexpr (!PAIR)
+            if (tw < ntile) dt.loadB(a, 0, tb);
     }
-    const unsigned long long tm = rtime(a.trace);
-    if (a.diag & 8) {  // staging only
-        trace_wave(a.trace, blockIdx.x * NW + w, t0, tm);
-        return;
+    const unsigned long long tm = PAIR ? 0ull : rtime(a.trace);
+    if (!PAIR && (a.diag & 8)) {  // staging only
+        trace_wave(a.trace, idx * NW + w, t0, tm);
+        return false;
     }
-    if (tw < ntile) dt.run(a, As, tb);
-    const unsigned long long td = rtime(a.trace);
+    if constexpr (!PAIR)
+        if (tw < ntile) dt.run(a, As, tb);
+    const unsigned long long td = PAIR ? 0ull : rtime(a.trace);
     // later phases (items with more pieces than row-groups, e.g. short column runs): phase ph
     // runs the column window [ph NG, (ph + 1) NG) of the item's pieces (longest first inside;
     // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
@@ -883,54 +935,60 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         pn.len = 0;
         if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
     };
-    if (NG < np)
-        fetch(1);
-    else
-        load_runs();
+    if (NG < np) fetch(1);
     if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     for (u32 ph = 1; ph * NG < np; ++ph) {
         pc = pn;
 #pragma unroll
         for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
-        if ((ph + 1) * NG < np)
-            fetch(ph + 1);
-        else
-            load_runs();
+        if ((ph + 1) * NG < np) fetch(ph + 1);
         if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
     }
-    for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
-        dt.load(a, a.tileIds[t], q0, tb);
-        dt.run(a, As, tb);
+    // (behind the pieces, not in their last phase: live across the phase loop, the descriptors
+    // cost the loop VGPRs; a wave that ends early has them back before the store-pass barrier)
+    load_runs();
+    if constexpr (!PAIR) {
+        for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
+            dt.load(a, a.tileIds[t], q0, tb);
+            dt.run(a, As, tb);
+        }
     }
+    bool staged_next = false;
     if (a.outLds) {  // the item's results in CSR order: runs of consecutive positions
         __syncthreads();
-        const uint2 ie = a.itemEnt[blockIdx.x];
+        const uint2 ie = a.itemEnt[idx];
         const float* res = reinterpret_cast<const float*>(As + a.outLds);
-        if (!(a.diag & 128)) {  // (BSMR_DIAG & 128, ablation only: no P stores)
-            // eight position loads in flight per lane before their stores: a loop of dependent
-            // load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5: 1.135 ->
-            // 1.082 ms). Issuing the first batch before the barrier measured slower (1.109 ms)
-            constexpr u32 U = 8;
-            auto pass = [&]() {
-                for (u32 t0 = tid; t0 < ie.y; t0 += U * NT) {
-                    u32 pos[U];
+        const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
+        if constexpr (PAIR && ROWV) {
+            // pairs: this wave's run values into registers, a barrier (no wave reads a slot
+            // any more), the next item's LDS-DMAs (their filler blocks overwrite the slots),
+            // then this item's stores, all in flight together
+            if (has_next && __builtin_amdgcn_readfirstlane(irun.y) <= NW * PAIR_RUNS_PER_WAVE) {
+                float v[PAIR_RUNS_PER_WAVE];
 #pragma unroll
-                    for (u32 k = 0; k < U; ++k) {
-                        const u32 t = t0 + k * NT;
-                        pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
-                    }
-#pragma unroll
-                    for (u32 k = 0; k < U; ++k) {
-                        const u32 t = t0 + k * NT;
-                        if (t < ie.y) a.P[pos[k]] = res[t];
-                    }
+                for (u32 u = 0; u < PAIR_RUNS_PER_WAVE; ++u) {
+                    const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), u));
+                    const u32 len = u < nr ? sl >> 16 : 0u;
+                    v[u] = lane < len ? res[(sl & 0xFFFFu) + lane] : 0.0f;
                 }
-            };
-            if (a.runs) {
+                __syncthreads();
+                rowv = rown;
+                stage(std::integral_constant<int, 0>{});
+#pragma unroll
+                for (u32 u = 0; u < PAIR_RUNS_PER_WAVE; ++u) {
+                    const u32 pos = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), u));
+                    const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), u));
+                    const u32 len = u < nr ? sl >> 16 : 0u;
+                    if (lane < len) a.P[pos + lane] = v[u];
+                }
+                return true;
+            }
+        }
+        if (PAIR || !(a.diag & 128)) {  // (BSMR_DIAG & 128, ablation only: no P stores)
+            if (PAIR || a.runs) {
                 // wave w writes runs w, w + NW, ...: one contiguous store of up to 64 results
                 // per run (a row's results in this item, when rows are column-sorted), four
                 // runs per step with their LDS reads in flight together
-                const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
                 for (u32 i = 0; i < nr; i += 4) {
                     u32 pos[4], s0[4], len[4];
                     float v[4];
@@ -947,12 +1005,63 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                     for (u32 u = 0; u < 4; ++u)  // (runs are at most 64 long)
                         if (lane < len[u]) a.P[pos[u] + lane] = v[u];
                 }
-            } else {
-                pass();
+            } else if constexpr (!PAIR) {
+                // eight position loads in flight per lane before their stores: a loop of
+                // dependent load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5:
+                // 1.135 -> 1.082 ms). Issuing the first batch before the barrier measured slower
+                constexpr u32 U = 8;
+                for (u32 t0s = tid; t0s < ie.y; t0s += U * NT) {
+                    u32 pos[U];
+#pragma unroll
+                    for (u32 k = 0; k < U; ++k) {
+                        const u32 t = t0s + k * NT;
+                        pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
+                    }
+#pragma unroll
+                    for (u32 k = 0; k < U; ++k) {
+                        const u32 t = t0s + k * NT;
+                        if (t < ie.y) a.P[pos[k]] = res[t];
+                    }
+                }
+            }
+        }
+        // a pair whose first item stored the plain way: the next image is staged now (every
+        // slot read has completed at the barrier)
+        if constexpr (PAIR && ROWV) {
+            if (has_next) {
+                __syncthreads();
+                rowv = rown;
+                stage(std::integral_constant<int, 0>{});
+                staged_next = true;
             }
         }
     }
-    trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
+    if constexpr (!PAIR) trace_wave(a.trace, idx * NW + w, t0, tm, td);
+    return staged_next;
+}
+
+// Row-block SDDMM: one workgroup per work item {row block, kept-tile range, piece
+// range}: the row block's A rows staged in LDS, then its MFMA tiles and column-run pieces. With
+// a.pairs (staged output by runs) a workgroup runs two consecutive items of its XCD's list, the
+// second one's staging overlapping the first one's store pass.
+template <int DT, int RBY, int NT, bool PAIR>
+__global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char AsB[];
+    char* As = AsB;
+    if (blockIdx.y) {  // batch b (item -> XCD placement unchanged: nItems is a multiple of 8)
+        a.A += blockIdx.y * a.bA;
+        a.B += blockIdx.y * a.bB;
+        a.P += blockIdx.y * a.bP;
+    }
+    if constexpr (!PAIR) {
+        rb_item<DT, RBY, NT, false>(a, As, blockIdx.x, false, NO_ITEM);
+    } else {
+        // list positions 2j and 2j + 1 of XCD x (items are laid out [position * 8 + x]);
+        // workgroup g runs on XCD g % 8
+        const u32 x = blockIdx.x % XCD_BUCKETS, i0 = (blockIdx.x / XCD_BUCKETS) * 2 * XCD_BUCKETS + x;
+        if (rb_item<DT, RBY, NT, true>(a, As, i0, false, i0 + XCD_BUCKETS))
+            rb_item<DT, RBY, NT, true>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
+    }
 }
 
 static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
@@ -1089,6 +1198,12 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.itemEnt = L.itemEnt.data();
     a.runs = L.outRuns ? L.runs.data() : nullptr;
     a.itemRuns = L.outRuns ? L.itemRuns.data() : nullptr;
+    // pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 256 bytes, an even number
+    // of list positions per XCD; not under the profiling ablations that cut an item short
+    a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 256 && L.nTilesKept == 0 &&
+                      L.nItems % (2 * XCD_BUCKETS) == 0 && !a.stageNt && a.lateB && p.diag == 0
+                  ? 1u
+                  : 0u;
     a.tilePanel = p.denseItems.data();
     a.tileIds = L.tileIds.data();
     a.denseCols = p.denseCols.data();
@@ -1103,7 +1218,9 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY) (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>)
+#define BSMR_RB(DT, RBY)                                                                  \
+    (a.pairs ? (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true> : k_sddmm_rb<DT, RBY, 512, true>) \
+             : (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false> : k_sddmm_rb<DT, RBY, 512, false>))
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
@@ -1118,7 +1235,8 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
 #undef BSMR_RB2
 #undef BSMR_RB
     // k_sddmm_rb stages a fixed 160 / 80 KiB per workgroup (the image and an unused tail)
-    hipLaunchKernelGGL(fn, dim3(L.nItems, nb), dim3(L.NT), (L.NT == 1024 ? 160 : 80) * 1024, s, a);
+    hipLaunchKernelGGL(fn, dim3(a.pairs ? L.nItems / 2 : L.nItems, nb), dim3(L.NT),
+                       (L.NT == 1024 ? 160 : 80) * 1024, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }
