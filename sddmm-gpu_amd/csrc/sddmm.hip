@@ -762,9 +762,12 @@ __device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const 
 // slots have been read into registers, so the next image lands while this item's stores drain.
 // Returns whether next's staging was issued (false: next is padding, or this item holds more
 // runs per wave than PAIR_RUNS_PER_WAVE and stored them the plain way).
-template <int DT, int RBY, int NT, bool PAIR>
+template <int DT, int RBY, int NT, int OM>
 __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx, const bool prestaged,
                                         const u32 next) {
+    // OM (output mode): 0 = one store per entry (a.outLds == 0), 1 = staged output (slots in
+    // LDS, written per item in CSR order), 2 = staged output by runs in pairs (PAIR)
+    constexpr bool PAIR = OM == 2, STAGED = OM != 0;
     using Geo = RowGeom<RBY>;
     constexpr u32 G = Geo::G, NC = Geo::NC;  // lanes per entry, chunks per lane
     constexpr u32 NW = NT / 64;               // waves per workgroup
@@ -860,7 +863,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     uint2 myrun = make_uint2(0u, 0u), irun = make_uint2(0u, 0u);
     u32 rown = a.row0;
     auto load_runs = [&]() {
-        if (a.runs && a.outLds) {
+        if (STAGED && a.runs && a.outLds) {
             irun = a.itemRuns[idx];
             irun.x = __builtin_amdgcn_readfirstlane(irun.x);
             irun.y = __builtin_amdgcn_readfirstlane(irun.y);
@@ -946,7 +949,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     }
     // (behind the pieces, not in their last phase: live across the phase loop, the descriptors
     // cost the loop VGPRs; a wave that ends early has them back before the store-pass barrier)
-    load_runs();
+    if constexpr (STAGED) load_runs();
     if constexpr (!PAIR) {
         for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
             dt.load(a, a.tileIds[t], q0, tb);
@@ -954,7 +957,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
         }
     }
     bool staged_next = false;
-    if (a.outLds) {  // the item's results in CSR order: runs of consecutive positions
+    if (STAGED && a.outLds) {  // the item's results in CSR order: runs of consecutive positions
         __syncthreads();
         const uint2 ie = a.itemEnt[idx];
         const float* res = reinterpret_cast<const float*>(As + a.outLds);
@@ -1044,7 +1047,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
 // range}: the row block's A rows staged in LDS, then its MFMA tiles and column-run pieces. With
 // a.pairs (staged output by runs) a workgroup runs two consecutive items of its XCD's list, the
 // second one's staging overlapping the first one's store pass.
-template <int DT, int RBY, int NT, bool PAIR>
+template <int DT, int RBY, int NT, int OM>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char AsB[];
     char* As = AsB;
@@ -1053,15 +1056,27 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         a.B += blockIdx.y * a.bB;
         a.P += blockIdx.y * a.bP;
     }
-    if constexpr (!PAIR) {
-        rb_item<DT, RBY, NT, false>(a, As, blockIdx.x, false, NO_ITEM);
+    if constexpr (OM != 2) {
+        rb_item<DT, RBY, NT, OM>(a, As, blockIdx.x, false, NO_ITEM);
     } else {
         // list positions 2j and 2j + 1 of XCD x (items are laid out [position * 8 + x]);
         // workgroup g runs on XCD g % 8
         const u32 x = blockIdx.x % XCD_BUCKETS, i0 = (blockIdx.x / XCD_BUCKETS) * 2 * XCD_BUCKETS + x;
-        if (rb_item<DT, RBY, NT, true>(a, As, i0, false, i0 + XCD_BUCKETS))
-            rb_item<DT, RBY, NT, true>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
+        if (rb_item<DT, RBY, NT, 2>(a, As, i0, false, i0 + XCD_BUCKETS))
+            rb_item<DT, RBY, NT, 2>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
     }
+}
+
+template <int DT, int RBY>
+void (*pick_rb(const u32 NT, const int om))(RbArgs) {
+    static_assert(RBY >= 128, "row sizes 128 .. 2048 bytes");
+    if constexpr (RBY == 128) {  // (no pairs: launch_rb enables them from 256-byte rows)
+        if (NT == 1024) return om == 0 ? k_sddmm_rb<DT, RBY, 1024, 0> : k_sddmm_rb<DT, RBY, 1024, 1>;
+        return om == 0 ? k_sddmm_rb<DT, RBY, 512, 0> : k_sddmm_rb<DT, RBY, 512, 1>;
+    }
+    if (NT == 1024)
+        return om == 0 ? k_sddmm_rb<DT, RBY, 1024, 0> : om == 1 ? k_sddmm_rb<DT, RBY, 1024, 1> : k_sddmm_rb<DT, RBY, 1024, 2>;
+    return om == 0 ? k_sddmm_rb<DT, RBY, 512, 0> : om == 1 ? k_sddmm_rb<DT, RBY, 512, 1> : k_sddmm_rb<DT, RBY, 512, 2>;
 }
 
 static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
@@ -1218,9 +1233,8 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY)                                                                  \
-    (a.pairs ? (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true> : k_sddmm_rb<DT, RBY, 512, true>) \
-             : (L.NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false> : k_sddmm_rb<DT, RBY, 512, false>))
+    const int om = !a.outLds ? 0 : a.pairs ? 2 : 1;
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, om)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
