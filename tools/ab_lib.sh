@@ -1,9 +1,10 @@
 #!/bin/bash
 # A/B timing of two builds of libbsmr_amd.so (through gpurun): the in-tree lib vs $2 (a variant
 # build, e.g. sddmm-gpu_amd/lib_exp/libbsmr_amd.so), alternating, on the listed configs.
-#   bash tools/ab_lib.sh <tag> <variant.so> "C4 C3 C2"
+#   bash tools/ab_lib.sh <tag> <variant.so> "C4 C3 C2" [swap]   (swap: the variant runs first)
 set -o pipefail
-TAG=$1; VAR=$2; CFGS=${3:-"C4 C3 C2"}
+TAG=$1; VAR=$2; CFGS=${3:-"C4 C3 C2"}; ORDER="base var base var"
+[ "$4" = swap ] && ORDER="var base var base"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 for c in $CFGS; do
@@ -15,7 +16,7 @@ for c in $CFGS; do
         C5u) ARGS="--workload dlmc_like --mask uniform --K 512 --dtype bf16" ;;
         C5b) ARGS="--workload dlmc_like --mask block --K 512 --dtype bf16" ;;
     esac
-    for v in base var base var; do
+    for v in $ORDER; do
         if [ $v = var ]; then export BSMR_LIB_PATH=$VAR; else unset BSMR_LIB_PATH; fi
         timeout -k 10 300 python3 tools/prof_sddmm.py --iters 30 $ARGS > "$OUT/${c}_$v.json" 2> "$OUT/${c}_$v.err" || exit $?
         echo "$c $v $(python3 -c "import json; d=json.loads(open('$OUT/${c}_$v.json').read().strip().splitlines()[-1]); print(d['timing_ms']['total_ms'])")" | tee -a "$OUT/summary.txt"

@@ -15,7 +15,8 @@
 #   hybrid                  tools/hybrid_table.py (-t 1 logs of the five matrices + analyzer table)
 #   ab:VAR:v1,v2:cfg1,cfg2  tools/ab_env.sh: alternating A/B of one BSMR_* knob (VAR without the
 #                           prefix may list several, joined by '+') on ab_env.sh's configs
-#   ablib:<variant.so>:cfg1,cfg2   tools/ab_lib.sh: the in-tree library against a variant build
+#   ablib:<variant.so>:cfg1,cfg2[:swap]   tools/ab_lib.sh: the in-tree library against a variant
+#                           build (swap: the variant runs first in each pair)
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -62,8 +63,8 @@ run_step() {
         hybrid) timeout -k 10 1100 python3 -u tools/hybrid_table.py --run --out "$OUT/hybrid" > "$OUT/hybrid.log" 2>&1 ;;
         ab) IFS=: read -r _ var vals cfgs <<< "$s"
             timeout -k 10 1100 bash tools/ab_env.sh "$TAG/ab_${var//+/_}" "BSMR_${var//+/,BSMR_}" "${vals//,/ }" "${cfgs//,/ }" > "$OUT/$f.log" 2>&1 ;;
-        ablib) IFS=: read -r _ so cfgs <<< "$s"
-            timeout -k 10 1100 bash tools/ab_lib.sh "$TAG/ablib_$(basename "$so" .so)" "$so" "${cfgs//,/ }" > "$OUT/$f.log" 2>&1 ;;
+        ablib) IFS=: read -r _ so cfgs order <<< "$s"
+            timeout -k 10 1100 bash tools/ab_lib.sh "$TAG/ablib_$(basename "$so" .so)${order:+_$order}" "$so" "${cfgs//,/ }" $order > "$OUT/$f.log" 2>&1 ;;
         *) echo "unknown step $s" >&2; return 2 ;;
     esac
     local rc=$?
