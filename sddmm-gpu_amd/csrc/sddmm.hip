@@ -1044,10 +1044,12 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
 }
 
 // Row-block SDDMM: one workgroup per work item {row block, kept-tile range, piece
-// range}: the row block's A rows staged in LDS, then its MFMA tiles and column-run pieces. With
-// a.pairs (staged output by runs) a workgroup runs two consecutive items of its XCD's list, the
-// second one's staging overlapping the first one's store pass.
-template <int DT, int RBY, int NT, int OM>
+// range}: the row block's A rows staged in LDS, then its MFMA tiles and column-run pieces, then
+// (staged output) the item's results in CSR order.
+// (This single-item kernel keeps its own body rather than calling rb_item: the shared form
+// measured 3 % slower on C2, 10.70 vs 10.46 us on one box, with the same instruction count; the
+// pair kernel below uses rb_item.)
+template <int DT, int RBY, int NT>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char AsB[];
     char* As = AsB;
@@ -1056,27 +1058,259 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         a.B += blockIdx.y * a.bB;
         a.P += blockIdx.y * a.bP;
     }
-    if constexpr (OM != 2) {
-        rb_item<DT, RBY, NT, OM>(a, As, blockIdx.x, false, NO_ITEM);
+    using Geo = RowGeom<RBY>;
+    constexpr u32 G = Geo::G, NC = Geo::NC;  // lanes per entry, chunks per lane
+    constexpr u32 NW = NT / 64;               // waves per workgroup
+    constexpr u32 NG = NT / G;                // residual row-groups
+    constexpr u32 TC = DenseTileLds<DT, RBY>::CH;
+    const unsigned long long t0 = rtime(a.trace);
+    uint4 it = a.items[blockIdx.x];
+    // all four fields in SGPRs before the padding test: the compiler otherwise loads .x (the row
+    // block) in a second, dependent round trip after the test
+    it.x = __builtin_amdgcn_readfirstlane(it.x);
+    it.y = __builtin_amdgcn_readfirstlane(it.y);
+    it.z = __builtin_amdgcn_readfirstlane(it.z);
+    it.w = __builtin_amdgcn_readfirstlane(it.w);
+    const u32 pend = a.itemEnd[blockIdx.x];
+    if (it.y == it.z && it.w == pend) return;  // padding item (uniform across the workgroup)
+    const u32 q0 = a.qbase + it.x * a.RB;
+    const u32 tid = threadIdx.x, w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
+    // every wave takes (at most) one dense tile and its row-groups one residual piece each per
+    // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
+    // staging loads so all of it is in flight together
+    const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
+    const u32 np = (a.mode & 2) ? pend - it.w : 0u;
+    const u32 gr = tid / G;
+    u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
+#pragma unroll
+    for (u32 f = 0; f < NC; ++f) rot[f] = 16u * G * ((f + j % Geo::RR) % NC);
+    // stage the row block by LDS-DMA: each wave-instruction fills one contiguous KiB of the image
+    // (64 chunks of the row-major image); lane l supplies image chunk x = 64 b + l, i.e. row
+    // lr = x / NCH at physical chunk pc = x % NCH, read from the logical chunk lds_chunk(lr, pc)
+    // of A[rows[q0 + lr]] (the XOR is an involution). The row indices of the wave's blocks are
+    // loaded once, one per lane, and handed to the block's lanes with v_readlane + select.
+    // Every wave stages exactly MAXB blocks b = w + i NW (the launch's whole LDS: 160 KiB at 1024
+    // threads, 80 KiB at 512), unconditionally: blocks past the image land in its unused tail
+    // (their rows read A row 0). A branch around a block, or any LDS instruction between two
+    // LDS-DMAs (a ds_bpermute hand-out of the row indices did this), makes the compiler wait
+    // (vmcnt(0)) for each LDS-DMA before issuing the next, which serialised the staging
+    // (C2: 12.8 -> 12.0 us once removed).
+    constexpr u32 NCH = RBY / 16;
+    constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
+    constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
+    static_assert(MAXB * NW == (NT == 1024 ? 160u : 80u), "whole KiB blocks");
+    constexpr bool ROWV = MAXB * NR <= 64;  // one row index per lane (else 128-byte rows)
+    const u32 lane = tid & 63;
+    const u32 ws = __builtin_amdgcn_readfirstlane(w);  // wave index in an SGPR
+    // the staging row indices are loaded first: they depend only on the item, so their round
+    // trip overlaps the piece descriptor's, and the LDS-DMAs need not wait for the B columns
+    u32 rowv = a.row0;
+    u32 src[ROWV ? 1 : MAXB];
+    if constexpr (ROWV) {
+        const u32 i = lane / NR, b = ws + i * NW, lr = 64 * b / NCH + lane % NR, q = q0 + lr;
+        if (i < MAXB && lr < a.RB && q < a.R) rowv = a.rows[q];
     } else {
-        // list positions 2j and 2j + 1 of XCD x (items are laid out [position * 8 + x]);
-        // workgroup g runs on XCD g % 8
-        const u32 x = blockIdx.x % XCD_BUCKETS, i0 = (blockIdx.x / XCD_BUCKETS) * 2 * XCD_BUCKETS + x;
-        if (rb_item<DT, RBY, NT, 2>(a, As, i0, false, i0 + XCD_BUCKETS))
-            rb_item<DT, RBY, NT, 2>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
+        // 128-byte rows: 8 rows per block, too many indices for one per lane; each lane loads
+        // the row of its own chunk for every block
+#pragma unroll
+        for (u32 i = 0; i < MAXB; ++i) {
+            const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
+            src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
+        }
     }
+    // the loads the LDS-DMA issue waits for go first: row indices, the phase-0 piece descriptor
+    // and the first tile's metadata (one round trip together); the B columns and entry metadata
+    // they address are issued after the LDS-DMAs, so the staging never waits for a B gather
+    f32x4 tb[TC], pre[NC];
+    DenseTileLds<DT, RBY> dt;
+    // tiles go to the last waves, which hold the shortest pieces (pieces are sorted longest first)
+    const u32 tw = NW - 1 - w;
+    Piece<RBY> pc;
+    pc.len = 0;
+    if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
+    if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
+    // staged output by runs: this lane's run descriptor (run w + NW * lane of the item), loaded
+    // in the item's last piece phase, where the next-phase prefetch registers are free, so the
+    // store pass waits for nothing but the LDS slots
+    uint2 myrun = make_uint2(0u, 0u), irun = make_uint2(0u, 0u);
+    auto load_runs = [&]() {
+        if (a.runs && a.outLds) {
+            irun = a.itemRuns[blockIdx.x];
+            irun.x = __builtin_amdgcn_readfirstlane(irun.x);
+            irun.y = __builtin_amdgcn_readfirstlane(irun.y);
+            const u32 j = w + NW * lane;
+            if (j < irun.y) myrun = a.runs[irun.x + j];
+        }
+    };
+    // AUX: the LDS-DMA cache policy (0 default; 2 = nt, stream the A rows past the XCD's L2 so the
+    // B columns of the item's column range stay resident: large staged-output layouts, where an
+    // item's row block is not staged again on that XCD until the next range)
+    auto stage = [&](auto aux_tag) {
+        constexpr int AUX = decltype(aux_tag)::value;
+        // the source chunk of lane l is the same in every block of the wave: x % NCH and
+        // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
+        const u32 x0 = 64 * ws + lane;
+        const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
+        if constexpr (ROWV) {
+#pragma unroll
+            for (u32 i = 0; i < MAXB; ++i) {
+                const u32 b = ws + i * NW;
+                u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
+#pragma unroll
+                for (u32 k = 1; k < NR; ++k) {
+                    const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
+                    src = lane / NCH == k ? rk : src;
+                }
+                const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
+                                                 16, 0, AUX);
+            }
+        } else {
+#pragma unroll
+            for (u32 i = 0; i < MAXB; ++i) {
+                const u32 b = ws + i * NW;
+                const char* g = a.A + (static_cast<size_t>(src[i]) * RBY + coff);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
+                                                 16, 0, AUX);
+            }
+        }
+    };
+    if (a.stageNt)
+        stage(std::integral_constant<int, 2>{});
+    else
+        stage(std::integral_constant<int, 0>{});
+    // the phase-0 B columns and entry metadata: issued right behind the LDS-DMAs (so the
+    // barrier's wait covers them too), or with lateB after the barrier (the barrier then waits
+    // for the staging alone and the waves pay one load round trip before their first piece)
+    if (!a.lateB) {
+        if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
+        if (tw < ntile) dt.loadB(a, 0, tb);
+    }
+    // every LDS-DMA of the workgroup has landed before any wave reads the image or writes the
+    // staged-output slots (the blocks past the image land in the tail those slots use); explicit,
+    // not left to the compiler's wait insertion at the barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (a.lateB) {
+        if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
+        if (tw < ntile) dt.loadB(a, 0, tb);
+    }
+    const unsigned long long tm = rtime(a.trace);
+    if (a.diag & 8) {  // staging only
+        trace_wave(a.trace, blockIdx.x * NW + w, t0, tm);
+        return;
+    }
+    if (tw < ntile) dt.run(a, As, tb);
+    const unsigned long long td = rtime(a.trace);
+    // later phases (items with more pieces than row-groups, e.g. short column runs): phase ph
+    // runs the column window [ph NG, (ph + 1) NG) of the item's pieces (longest first inside;
+    // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
+    // alternates long and short pieces; phase ph's piece and B column are loaded while phase
+    // ph - 1 computes (two register sets)
+    Piece<RBY> pn;
+    f32x4 nb[NC];
+    auto fetch = [&](const u32 ph) {
+        const u32 pi = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
+        pn.len = 0;
+        if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
+    };
+    if (NG < np)
+        fetch(1);
+    else
+        load_runs();
+    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+    for (u32 ph = 1; ph * NG < np; ++ph) {
+        pc = pn;
+#pragma unroll
+        for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
+        if ((ph + 1) * NG < np)
+            fetch(ph + 1);
+        else
+            load_runs();
+        if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+    }
+    for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
+        dt.load(a, a.tileIds[t], q0, tb);
+        dt.run(a, As, tb);
+    }
+    if (a.outLds) {  // the item's results in CSR order: runs of consecutive positions
+        __syncthreads();
+        const uint2 ie = a.itemEnt[blockIdx.x];
+        const float* res = reinterpret_cast<const float*>(As + a.outLds);
+        if (!(a.diag & 128)) {  // (BSMR_DIAG & 128, ablation only: no P stores)
+            // eight position loads in flight per lane before their stores: a loop of dependent
+            // load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5: 1.135 ->
+            // 1.082 ms). Issuing the first batch before the barrier measured slower (1.109 ms)
+            constexpr u32 U = 8;
+            auto pass = [&]() {
+                for (u32 t0 = tid; t0 < ie.y; t0 += U * NT) {
+                    u32 pos[U];
+#pragma unroll
+                    for (u32 k = 0; k < U; ++k) {
+                        const u32 t = t0 + k * NT;
+                        pos[k] = t < ie.y ? a.sortedPos[ie.x + t] : 0u;
+                    }
+#pragma unroll
+                    for (u32 k = 0; k < U; ++k) {
+                        const u32 t = t0 + k * NT;
+                        if (t < ie.y) a.P[pos[k]] = res[t];
+                    }
+                }
+            };
+            if (a.runs) {
+                // wave w writes runs w, w + NW, ...: one contiguous store of up to 64 results
+                // per run (a row's results in this item, when rows are column-sorted), four
+                // runs per step with their LDS reads in flight together
+                const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
+                for (u32 i = 0; i < nr; i += 4) {
+                    u32 pos[4], s0[4], len[4];
+                    float v[4];
+#pragma unroll
+                    for (u32 u = 0; u < 4; ++u) {
+                        const u32 q = min(i + u, 63u);
+                        pos[u] = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), q));
+                        const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), q));
+                        s0[u] = sl & 0xFFFFu;
+                        len[u] = i + u < nr ? sl >> 16 : 0u;
+                        v[u] = lane < len[u] ? res[s0[u] + lane] : 0.0f;
+                    }
+#pragma unroll
+                    for (u32 u = 0; u < 4; ++u)  // (runs are at most 64 long)
+                        if (lane < len[u]) a.P[pos[u] + lane] = v[u];
+                }
+            } else {
+                pass();
+            }
+        }
+    }
+    trace_wave(a.trace, blockIdx.x * NW + w, t0, tm, td);
+}
+
+// Pairs (staged output by runs): a workgroup runs list positions 2j and 2j + 1 of its XCD
+// (items are laid out [position * 8 + x]; workgroup g runs on XCD g % 8), the second item's
+// staging issued in the first one's store pass (rb_item)
+template <int DT, int RBY, int NT>
+__global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char AsB[];
+    char* As = AsB;
+    if (blockIdx.y) {  // batch b
+        a.A += blockIdx.y * a.bA;
+        a.B += blockIdx.y * a.bB;
+        a.P += blockIdx.y * a.bP;
+    }
+    const u32 x = blockIdx.x % XCD_BUCKETS, i0 = (blockIdx.x / XCD_BUCKETS) * 2 * XCD_BUCKETS + x;
+    if (rb_item<DT, RBY, NT, 2>(a, As, i0, false, i0 + XCD_BUCKETS))
+        rb_item<DT, RBY, NT, 2>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
 }
 
 template <int DT, int RBY>
-void (*pick_rb(const u32 NT, const int om))(RbArgs) {
-    static_assert(RBY >= 128, "row sizes 128 .. 2048 bytes");
-    if constexpr (RBY == 128) {  // (no pairs: launch_rb enables them from 256-byte rows)
-        if (NT == 1024) return om == 0 ? k_sddmm_rb<DT, RBY, 1024, 0> : k_sddmm_rb<DT, RBY, 1024, 1>;
-        return om == 0 ? k_sddmm_rb<DT, RBY, 512, 0> : k_sddmm_rb<DT, RBY, 512, 1>;
+void (*pick_rb(const u32 NT, const bool pairs))(RbArgs) {
+    if constexpr (RBY >= 256) {  // (no pairs at 128-byte rows: launch_rb enables them from 256)
+        if (pairs) return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024> : k_sddmm_rb_pair<DT, RBY, 512>;
     }
-    if (NT == 1024)
-        return om == 0 ? k_sddmm_rb<DT, RBY, 1024, 0> : om == 1 ? k_sddmm_rb<DT, RBY, 1024, 1> : k_sddmm_rb<DT, RBY, 1024, 2>;
-    return om == 0 ? k_sddmm_rb<DT, RBY, 512, 0> : om == 1 ? k_sddmm_rb<DT, RBY, 512, 1> : k_sddmm_rb<DT, RBY, 512, 2>;
+    return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>;
 }
 
 static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
@@ -1233,8 +1467,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-    const int om = !a.outLds ? 0 : a.pairs ? 2 : 1;
-#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, om)
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
