@@ -419,15 +419,34 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
 #pragma unroll
         for (u32 q = 0; q < NX / 4; ++q)
             if (256 * (q + 1) < nb) chunk(ent[4 * q], ent[4 * q + 1], ent[4 * q + 2], ent[4 * q + 3]);
-        for (u32 e0 = l + 256 + 64 * NX; e0 < nb; e0 += 256) {  // longer rows
-            u32 x[4];
+        // longer rows: one chunk in flight ahead of the one computed (the loop used to load a
+        // chunk and wait for it, one round trip per 256 entries)
+        auto load4 = [&](u32 (&x)[4], const u32 e0) {
 #pragma unroll
-            for (u32 u = 0; u < 4; ++u) {
+            for (u32 u = 0; u < 4; ++u) {  // clamped loads, no branch per load
                 const u32 e = e0 + 64 * u;
                 const u32 v = a.enc[b0 + min(e, nb - 1)];
                 x[u] = e < nb ? v : 0u;
             }
-            chunk(x[0], x[1], x[2], x[3]);
+        };
+        constexpr u32 C1 = 256 + 64 * NX;  // first entry past the prefetched chunks
+        if constexpr (TS > 4) {  // (the pipelined loop spills at T = 6 / 8)
+            for (u32 e0 = l + C1; e0 < nb; e0 += 256) {
+                u32 x[4];
+                load4(x, e0);
+                chunk(x[0], x[1], x[2], x[3]);
+            }
+        } else if (C1 < nb) {
+            u32 x[4];
+            load4(x, l + C1);
+            for (u32 c0 = C1; c0 < nb; c0 += 256) {  // wave-uniform chunk base
+                u32 y[4] = {0u, 0u, 0u, 0u};
+                const bool more = c0 + 256 < nb;
+                if (more) load4(y, l + c0 + 256);
+                chunk(x[0], x[1], x[2], x[3]);
+#pragma unroll
+                for (u32 u = 0; u < 4; ++u) x[u] = y[u];
+            }
         }
         red = wave_sum8(mn);
     }
@@ -2133,7 +2152,8 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     // tile of T clusters: as many representatives as fit the LDS budget, at most CL_TMAX, an
     // even number (block b of cluster c at reps[b * T + c]: 8- or 16-byte LDS reads of all T)
     const u32 NP = (nbpr + 3) & ~3u;
-    const u32 T = std::max<u32>(2, std::min<u32>(CL_TMAX, CL_LDS_BUDGET / (NP * 4)) & ~1u);
+    u32 T = std::max<u32>(2, std::min<u32>(CL_TMAX, CL_LDS_BUDGET / (NP * 4)) & ~1u);
+    if (diag & 65536) T = std::min<u32>(T, 4);  // (experiment: 4 clusters per tile)
     ca.NP = NP;
     ca.T = T;
     const size_t lds_cl = static_cast<size_t>(T) * NP * 4 + sizeof(ClusterCtl);

@@ -787,7 +787,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     const u32 pend = a.itemEnd[idx];
     if (it.y == it.z && it.w == pend) return false;  // padding item (uniform across the workgroup)
     // the next item of the pair: its row block (its staging rows are loaded in the last phase)
-    bool has_next = false;
+    bool has_next = false, same_rb = false;
     u32 q0n = 0;
     if (next != NO_ITEM) {
         uint4 nt = a.items[next];
@@ -798,6 +798,9 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
         const u32 nend = __builtin_amdgcn_readfirstlane(a.itemEnd[next]);
         has_next = !(nt.y == nt.z && nt.w == nend);
         q0n = a.qbase + nt.x * a.RB;
+        // the same row block (consecutive chunks of one segment): its image is already in LDS
+        // (the pieces only read it; the slots live past it), so nothing is staged again
+        same_rb = nt.x == it.x;
     }
     const u32 q0 = a.qbase + it.x * a.RB;
     const u32 tid = threadIdx.x, w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
@@ -871,7 +874,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
             if (jr < irun.y) myrun = a.runs[irun.x + jr];
         }
         if constexpr (ROWV)
-            if (has_next) rown = rb_stage_rows<RBY, NT>(a, q0n, ws, lane);
+            if (has_next && !same_rb) rown = rb_stage_rows<RBY, NT>(a, q0n, ws, lane);
     };
     // AUX: the LDS-DMA cache policy (0 default; 2 = nt, stream the A rows past the XCD's L2 so the
     // B columns of the item's column range stay resident: large staged-output layouts, where an
@@ -976,7 +979,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
                 }
                 __syncthreads();
                 rowv = rown;
-                stage(std::integral_constant<int, 0>{});
+                if (!same_rb) stage(std::integral_constant<int, 0>{});
 #pragma unroll
                 for (u32 u = 0; u < PAIR_RUNS_PER_WAVE; ++u) {
                     const u32 pos = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), u));
@@ -1034,7 +1037,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
             if (has_next) {
                 __syncthreads();
                 rowv = rown;
-                stage(std::integral_constant<int, 0>{});
+                if (!same_rb) stage(std::integral_constant<int, 0>{});
                 staged_next = true;
             }
         }

@@ -7,6 +7,7 @@
 #   tests:<a+b+...>         pytest -m gpu -k 'a or b or ...'
 #   bench:<cfg>             bench.py line of one config (C1 C2 C3 C4 C4x1 C5u C5b C2k32 C2k512)
 #   quick:<cfg>             the same without the CPU / vendor legs and PMC passes
+#   pmc:<cfg>               the same without the CPU / vendor legs, with the in-run PMC traffic
 #   rocprof:<cfg>           rocprofv3 --kernel-trace --stats of that config's bench (every traced
 #                           launch a timed step)
 #   strong:<scale>          bench's multi-GPU path on one GPU under torchrun (RCCL, world 1) with
@@ -15,6 +16,8 @@
 #   hybrid                  tools/hybrid_table.py (-t 1 logs of the five matrices + analyzer table)
 #   ab:VAR:v1,v2:cfg1,cfg2  tools/ab_env.sh: alternating A/B of one BSMR_* knob (VAR without the
 #                           prefix may list several, joined by '+') on ab_env.sh's configs
+#   planab:<scale>:d1,d2,...  reddit-like plan build (tools/plan_time.py) under each BSMR_DIAG value
+#                           in turn (permutation hash and clustering ms per run)
 #   ablib:<variant.so>:cfg1,cfg2[:swap]   tools/ab_lib.sh: the in-tree library against a variant
 #                           build (swap: the variant runs first in each pair)
 set -o pipefail
@@ -54,6 +57,7 @@ run_step() {
             fi ;;
         bench) timeout -k 10 900 python3 bench.py $(cfg_args "$arg") > "$OUT/bench_$arg.json" 2> "$OUT/bench_$arg.err" ;;
         quick) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") $QUICK > "$OUT/quick_$arg.json" 2> "$OUT/quick_$arg.err" ;;
+        pmc) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") --no-cpu-baseline --no-vendor --pmc on > "$OUT/pmc_$arg.json" 2> "$OUT/pmc_$arg.err" ;;
         rocprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$arg" -o run -- \
                      python3 bench.py $(cfg_args "$arg") $QUICK --no-split > "$OUT/rocprof_$arg.json" 2> "$OUT/rocprof_$arg.err" ;;
         strong) timeout -k 10 1000 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
@@ -65,6 +69,11 @@ run_step() {
             timeout -k 10 1100 bash tools/ab_env.sh "$TAG/ab_${var//+/_}" "BSMR_${var//+/,BSMR_}" "${vals//,/ }" "${cfgs//,/ }" > "$OUT/$f.log" 2>&1 ;;
         ablib) IFS=: read -r _ so cfgs order <<< "$s"
             timeout -k 10 1100 bash tools/ab_lib.sh "$TAG/ablib_$(basename "$so" .so)${order:+_$order}" "$so" "${cfgs//,/ }" $order > "$OUT/$f.log" 2>&1 ;;
+        planab) IFS=: read -r _ scale diags <<< "$s"
+            for d in ${diags//,/ }; do
+                BSMR_DIAG=$d timeout -k 10 300 python3 tools/plan_time.py --workload reddit_like --scale "$scale" --batches 16384 > "$OUT/plan_${scale}_$d.json" 2>> "$OUT/$f.log" || return $?
+                python3 -c "import json; d=json.load(open('$OUT/plan_${scale}_$d.json')); r=list(d['runs'].values())[0]; print('scale $scale diag $d', r['row_reorder_ms'], r['rows_sha256'], r['num_clusters'], r['wall_s'])" >> "$OUT/planab_summary.txt"
+            done ;;
         *) echo "unknown step $s" >&2; return 2 ;;
     esac
     local rc=$?

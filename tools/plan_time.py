@@ -22,7 +22,9 @@ def main():
     args = ap.parse_args()
     import numpy as np
 
-    from bsmr import Plan, synth
+    from bsmr import Plan, set_default_tuning, synth, tuning_from_env
+
+    set_default_tuning(tuning_from_env())  # BSMR_* knobs (A/B runs)
 
     gen = getattr(synth, args.workload)
     M, N, rp, ci = gen(args.scale) if args.scale is not None else gen()
