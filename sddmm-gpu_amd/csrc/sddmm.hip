@@ -1451,9 +1451,11 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.runs = L.outRuns ? L.runs.data() : nullptr;
     a.itemRuns = L.outRuns ? L.itemRuns.data() : nullptr;
     // pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 256 bytes, an even number
-    // of list positions per XCD; not under the profiling ablations that cut an item short
+    // of list positions per XCD; not under the profiling ablations (trace, staging only, B in
+    // L2, no stores)
     a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 256 && L.nTilesKept == 0 &&
-                      L.nItems % (2 * XCD_BUCKETS) == 0 && !a.stageNt && a.lateB && p.diag == 0
+                      L.nItems % (2 * XCD_BUCKETS) == 0 && !a.stageNt && a.lateB &&
+                      !(p.diag & (8u | 32u | 64u | 128u | 16384u))
                   ? 1u
                   : 0u;
     a.tilePanel = p.denseItems.data();
