@@ -85,6 +85,8 @@ def parse():
                          "(bsmr_plan_shard_rebalance) before the timed steps")
     ap.add_argument("--strong-scale", type=float, default=1.0,
                     help="reddit-like size of the strong_C4 block (1 = 232 M stored entries)")
+    ap.add_argument("--graph", action="store_true",
+                    help="also time the steps captured into one HIP graph (graph_replay block)")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -609,6 +611,33 @@ def main_single(args):
     ms = e0.elapsed_time(e1)
     ms_per_step = ms / args.steps
 
+    # the same K steps captured once into a HIP graph (torch.cuda.CUDAGraph on a side stream:
+    # hipStreamBeginCapture sees the library's launches on that stream) and replayed between
+    # events: what the per-launch host / dispatch overhead costs the stream-launched steps
+    graph = None
+    if args.graph and not args.no_split:
+        gs = torch.cuda.Stream(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(gs):
+            with torch.cuda.graph(g, stream=gs):
+                for _ in range(args.steps):
+                    plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=gs.cuda_stream,
+                               dtype=dtype)
+            g.replay()  # warm-up replay
+            gs.synchronize()
+            g0 = torch.cuda.Event(enable_timing=True)
+            g1 = torch.cuda.Event(enable_timing=True)
+            g0.record(gs)
+            g.replay()
+            g1.record(gs)
+            gs.synchronize()
+        gms = g0.elapsed_time(g1) / args.steps
+        graph = {"ms_per_step": round(gms, 5),
+                 "value": round(2.0 * nnz * K / (gms * 1e-3) / 1e9, 2), "steps": args.steps,
+                 "note": "the timed steps captured into one HIP graph and replayed (not the "
+                         "line's value: stream launches)"}
+        del g
+
     # cold: before each step a 512 MiB write evicts the Infinity Cache (MALL) and the L2s, so
     # A, B and the plan come from HBM; only the SDDMM launch is inside the events
     cold_ms = None
@@ -709,6 +738,8 @@ def main_single(args):
             and nnz <= 20_000_000):
         out["mfma"]["forced_tiles_split"] = forced_mfma_split(
             args, (M, N, rp, ci), K, dtype, dA, dB, dev, stream, P_gpu, flops_rank)
+    if graph is not None:
+        out["graph_replay"] = graph
     if cold_ms is not None:
         out["cold"] = {"ms_per_step": round(cold_ms, 5),
                        "value": round(flops_rank * world / (cold_ms * 1e-3) / 1e9, 2),

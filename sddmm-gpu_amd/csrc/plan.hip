@@ -1760,11 +1760,6 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     auto emit = [&](u32 xl, u32 b, u32 e0, u32 ne, u32 t0, u32 nt, u32 nch, double rcost) {
         if (staged) nch = std::max<u32>(nch, (ne + outCap - 1) / outCap);
         cuts_by_cost(e0, ne, nch, rcost);
-        // staged output: an even number of chunks per emitted range, so the launch's pairs
-        // (list positions 2j, 2j + 1, sddmm.hip k_sddmm_rb_pair) fall inside one row block and the
-        // second item reuses the first one's LDS image (BSMR_DIAG & 131072: as cut)
-        if (staged && !(diag & 131072) && (ecut.size() - 1) % 2 == 1 && ne >= 2)
-            cuts_by_cost(e0, ne, static_cast<u32>(ecut.size()), rcost);
         nch = static_cast<u32>(ecut.size() - 1);
         for (u32 k = 0; k < nch; ++k) {
             const u32 ea = ecut[k];
