@@ -85,8 +85,9 @@ def parse():
                          "(bsmr_plan_shard_rebalance) before the timed steps")
     ap.add_argument("--strong-scale", type=float, default=1.0,
                     help="reddit-like size of the strong_C4 block (1 = 232 M stored entries)")
-    ap.add_argument("--graph", action="store_true",
-                    help="also time the steps captured into one HIP graph (graph_replay block)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time the steps as stream launches only (default: the K timed steps "
+                         "captured into one HIP graph and replayed; both are reported)")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -133,6 +134,38 @@ def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200):
         ok = len(times) >= window and max(last) <= (1.0 + tol) * min(last)
         if ok or len(times) >= max_runs or (len(times) >= window and time.perf_counter() > t_end):
             return statistics.median(last), times, ok
+
+
+def graph_time(launch, steps, dev):
+    """ms per step of `steps` launches captured into one HIP graph and replayed (one warm-up
+    replay, then one timed replay between HIP events on the replay stream). launch(stream_handle)
+    issues one step on the given stream. A graph replay submits the K kernels without a host call
+    per launch (the MI355X-native form of a launch-bound loop; at ~10 us per C2 step the ctypes +
+    hipLaunchKernel path per step is as long as the kernel). Returns (ms, None), or (None,
+    reason) when capture fails (the caller then keeps the stream-launched time)."""
+    import torch
+
+    try:
+        gs = torch.cuda.Stream(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(gs):
+            with torch.cuda.graph(g, stream=gs):
+                for _ in range(steps):
+                    launch(gs.cuda_stream)
+            g.replay()  # warm-up replay
+            gs.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(gs)
+            g.replay()
+            e1.record(gs)
+            gs.synchronize()
+        ms = e0.elapsed_time(e1) / max(steps, 1)
+        del g
+        return ms, None
+    except Exception as e:  # noqa: BLE001 - reported; the stream-launched time stays
+        torch.cuda.synchronize()
+        return None, f"{type(e).__name__}: {e}"[:300]
 
 
 def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
@@ -611,32 +644,22 @@ def main_single(args):
     ms = e0.elapsed_time(e1)
     ms_per_step = ms / args.steps
 
-    # the same K steps captured once into a HIP graph (torch.cuda.CUDAGraph on a side stream:
-    # hipStreamBeginCapture sees the library's launches on that stream) and replayed between
-    # events: what the per-launch host / dispatch overhead costs the stream-launched steps
-    graph = None
-    if args.graph and not args.no_split:
-        gs = torch.cuda.Stream(dev)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(gs):
-            with torch.cuda.graph(g, stream=gs):
-                for _ in range(args.steps):
-                    plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=gs.cuda_stream,
-                               dtype=dtype)
-            g.replay()  # warm-up replay
-            gs.synchronize()
-            g0 = torch.cuda.Event(enable_timing=True)
-            g1 = torch.cuda.Event(enable_timing=True)
-            g0.record(gs)
-            g.replay()
-            g1.record(gs)
-            gs.synchronize()
-        gms = g0.elapsed_time(g1) / args.steps
-        graph = {"ms_per_step": round(gms, 5),
-                 "value": round(2.0 * nnz * K / (gms * 1e-3) / 1e9, 2), "steps": args.steps,
-                 "note": "the timed steps captured into one HIP graph and replayed (not the "
-                         "line's value: stream launches)"}
-        del g
+    stream_ms_per_step = ms_per_step
+    # the timed steps as one HIP graph (graph_time): the line's value when capture works,
+    # the stream-launched time beside it
+    graph_ms, graph_err = (None, "--no-graph") if args.no_graph else graph_time(
+        lambda h: plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=h, dtype=dtype),
+        args.steps, dev)
+    if graph_ms is not None:
+        ms_per_step = graph_ms
+    timing = {"method": "hip_graph" if graph_ms is not None else "stream_launches",
+              "graph_ms_per_step": round(graph_ms, 5) if graph_ms is not None else None,
+              "stream_launch_ms_per_step": round(stream_ms_per_step, 5),
+              "note": "value = the K timed steps captured into one HIP graph and replayed "
+                      "between HIP events (each step a full SDDMM launch); stream_launch = the "
+                      "same K steps launched one by one from Python"}
+    if graph_err:
+        timing["graph_error"] = graph_err
 
     # cold: before each step a 512 MiB write evicts the Infinity Cache (MALL) and the L2s, so
     # A, B and the plan come from HBM; only the SDDMM launch is inside the events
@@ -738,8 +761,7 @@ def main_single(args):
             and nnz <= 20_000_000):
         out["mfma"]["forced_tiles_split"] = forced_mfma_split(
             args, (M, N, rp, ci), K, dtype, dA, dB, dev, stream, P_gpu, flops_rank)
-    if graph is not None:
-        out["graph_replay"] = graph
+    out["timing"] = timing
     if cold_ms is not None:
         out["cold"] = {"ms_per_step": round(cold_ms, 5),
                        "value": round(flops_rank * world / (cold_ms * 1e-3) / 1e9, 2),
@@ -770,15 +792,28 @@ def sharded_workload(args, world):
                    "permutation, synth.stack_copies), one C2 per GPU", "weak")
 
 
-def _timed_steps(step, steps, warmup, stream):
-    """warmup untimed steps, then `steps` between HIP events on the launch stream, bracketed by a
-    barrier + device synchronisation on both sides; returns this rank's ms per step."""
+def _timed_steps(step, steps, warmup, stream, use_graph=True, has_work=True):
+    """warmup untimed steps, then `steps` timed, bracketed by a barrier + device synchronisation
+    on both sides; returns this rank's ms per step. step(h) issues one step on stream handle h
+    (default: the launch stream). Timed as one HIP graph of the `steps` launches (graph_time)
+    when use_graph and capture works on every rank, else (every rank) as stream launches between
+    HIP events. has_work = False: this rank launches nothing (0 ms)."""
     import torch
     import torch.distributed as dist
+
+    from bsmr import dist as D
 
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    if use_graph:
+        dist.barrier()
+        torch.cuda.synchronize()
+        ms, _ = graph_time(step, steps, stream.device) if has_work else (0.0, None)
+        torch.cuda.synchronize()
+        # the same method on every rank (the barriers below must pair up)
+        if min(D.all_values(1.0 if ms is not None else 0.0, stream.device)) > 0:
+            return ms
     dist.barrier()
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
@@ -863,13 +898,14 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
             dA_all = torch.from_numpy(A).to(dev).to(tdt)
             dP1 = torch.zeros(nnz, dtype=torch.float32, device=dev)
 
-            def whole():
-                plan.sddmm(dA_all.data_ptr(), dB.data_ptr(), K, dP1.data_ptr(), stream=sp,
+            def whole(h=sp):
+                plan.sddmm(dA_all.data_ptr(), dB.data_ptr(), K, dP1.data_ptr(), stream=h,
                            dtype=dtype)
         else:
-            def whole():
+            def whole(h=sp):
                 pass
-        whole_ms = _timed_steps(whole, args.steps, args.warmup, stream)
+        whole_ms = _timed_steps(whole, args.steps, args.warmup, stream, not args.no_graph,
+                                has_work=rank == 0)
         if rank == 0:
             del dA_all, dP1
             torch.cuda.empty_cache()
@@ -886,16 +922,17 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
         if cur["dA"].numel() == 0:
             cur["dA"] = torch.zeros(K, dtype=tdt, device=dev)
 
-    def step():
+    def step(h=sp):
         if cur["p1"] > cur["p0"]:
             plan.sddmm_panels_local(cur["dA"].data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
-                                    cur["p0"], cur["p1"], stream=sp, dtype=dtype)
+                                    cur["p0"], cur["p1"], stream=h, dtype=dtype)
 
     rounds = []
     best = None
     for it in range(args.rebalance + 1):
         use(cuts)
-        ms_r = D.all_values(_timed_steps(step, min(args.steps, 50), args.warmup, stream), dev)
+        ms_r = D.all_values(_timed_steps(step, min(args.steps, 50), args.warmup, stream,
+                                         not args.no_graph, cur["p1"] > cur["p0"]), dev)
         rounds.append({"cuts": [int(c) for c in cuts], "ms_per_step": [round(x, 5) for x in ms_r],
                        "imbalance_max_over_mean": round(max(ms_r) / (sum(ms_r) / world), 3)})
         if best is None or max(ms_r) < best[0]:
@@ -912,7 +949,8 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
     cuts = best[1]  # the fastest cut seen
     use(cuts)
     p0, p1 = cur["p0"], cur["p1"]
-    ms_mine = _timed_steps(step, args.steps, args.warmup, stream)
+    ms_mine = _timed_steps(step, args.steps, args.warmup, stream, not args.no_graph,
+                           cur["p1"] > cur["p0"])
     ms_all = D.all_values(ms_mine, dev)
     lens = np.diff(np.asarray(rp, dtype=np.int64))
     mine = int(lens[rows[16 * p0:min(16 * p1, len(rows))]].sum())
@@ -1004,11 +1042,12 @@ def shard_local(args, rank, world, wl, dev):
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    def step():
+    def step(h=sp):
         if plan:
-            plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP_loc.data_ptr(), stream=sp, dtype=dtype)
+            plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP_loc.data_ptr(), stream=h, dtype=dtype)
 
-    ms_mine = _timed_steps(step, args.steps, args.warmup, stream)
+    ms_mine = _timed_steps(step, args.steps, args.warmup, stream, not args.no_graph,
+                           plan is not None)
     if plan is None and e1 - e0 == 1:
         Ah = dA.float().cpu().numpy().reshape(-1)
         Bh = dB.float().cpu().numpy()
