@@ -193,7 +193,10 @@ struct ClusterArgs {
 
 constexpr double GUARD = 1e-5;
 constexpr u32 CL_TMAX = 8;      // clusters per tile (register arrays)
-constexpr u32 CL_WAVES = 16;    // waves per tile workgroup
+#ifndef BSMR_CL_WAVES
+#define BSMR_CL_WAVES 16
+#endif
+constexpr u32 CL_WAVES = BSMR_CL_WAVES;  // waves per tile workgroup
 #ifndef BSMR_CL_SUB
 #define BSMR_CL_SUB 64
 #endif
@@ -204,7 +207,10 @@ constexpr u32 CL_LDS_BUDGET = 148 * 1024;  // representatives (the control block
 // hands the rest of a sub-batch back to all waves
 constexpr u32 CL_LEADER_EVALS = 16;
 // encoding chunks (256 entries) of a row whose loads are issued together (registers: 4 per chunk)
-constexpr u32 CL_PRE_CH = 2;
+#ifndef BSMR_CL_PRE_CH
+#define BSMR_CL_PRE_CH 2
+#endif
+constexpr u32 CL_PRE_CH = BSMR_CL_PRE_CH;
 
 __device__ __forceinline__ u64 now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -407,7 +413,7 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
         // the row's first CL_PRE_CH chunks: chunk 0 was prefetched (pre), the next ones are all
         // issued now, so such a row pays one load round trip instead of one per chunk
         // (T = 8 keeps chunk 0 only: its 8 representatives' partial sums fill the registers)
-        constexpr u32 NX = TS <= 6 ? 4 * (CL_PRE_CH - 1) : 0;
+        constexpr u32 NX = TS <= 6 || CL_WAVES <= 8 ? 4 * (CL_PRE_CH - 1) : 0;
         u32 ent[NX > 0 ? NX : 1];
 #pragma unroll
         for (u32 u = 0; u < NX; ++u) {  // clamped loads, no branch per load
@@ -430,7 +436,7 @@ __device__ u32 eval_row(const ClusterArgs& a, const u32* reps, const ClusterCtl&
             }
         };
         constexpr u32 C1 = 256 + 64 * NX;  // first entry past the prefetched chunks
-        if constexpr (TS > 4) {  // (the pipelined loop spills at T = 6 / 8)
+        if constexpr (TS > 4 && CL_WAVES > 8) {  // (the pipelined loop spills at T = 6 / 8, 16 waves)
             for (u32 e0 = l + C1; e0 < nb; e0 += 256) {
                 u32 x[4];
                 load4(x, e0);
@@ -466,7 +472,7 @@ __device__ __forceinline__ void load_chunk0(const ClusterArgs& a, uint4 m, u32 (
 }
 
 template <u32 TS>
-__global__ __launch_bounds__(1024) void k_cluster(ClusterArgs a) {
+__global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
     extern __shared__ __attribute__((aligned(16))) u32 smem[];
     constexpr u32 T = TS;
     u32* reps = smem;  // [NP][TS]: block b of tile cluster c at reps[b * TS + c]
