@@ -384,10 +384,16 @@ def kernel_name(st, st_after, K, dtype, layout):
     if rby in (128, 256, 512, 1024, 2048) and layout != "colmajor" and not tile_dominated:
         tiles = ("fp32 tiles demoted to residual entries" if dtype == F32
                  else "dense-tile MFMA for tiles >= 128 entries")
-        rows = st_after["rb_rows"][{128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]]
+        i = {128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[rby]
+        rows = st_after["rb_rows"][i]
         nt = 1024 if rby * rows > 80 * 1024 else 512
-        return (f"k_sddmm_rb<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
-                f"rows per block: residual entries; {tiles})"), rby
+        # sddmm.hip launch_rb: staged output (P > 8 MiB) by runs, no kept MFMA tile, rows of
+        # >= 256 bytes -> the pair kernel (two list positions per workgroup)
+        pair = 4 * st["nnz"] > (8 << 20) and rby >= 256 and not st_after["rb_tiles"][i]
+        name = "k_sddmm_rb_pair" if pair else "k_sddmm_rb"
+        return (f"{name}<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
+                f"rows per block: residual entries; {tiles}"
+                f"{'; staged output by runs, two items per workgroup' if pair else ''})"), rby
     if dtype == F32:
         return f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)", rby
     return f"k_sddmm_half<{'f16' if dtype == 1 else 'bf16'}> (dense-tile MFMA + residual)", rby
