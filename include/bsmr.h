@@ -22,11 +22,11 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 7  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 8  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
                               the plan options (no environment reads in the library);
-                              7: bsmr_tuning.out_packed */
+                              7: bsmr_tuning.out_packed; 8: bsmr_tuning.sweep*, rb_sweep */
 
 typedef enum {
     BSMR_OK = 0,
@@ -127,6 +127,14 @@ typedef struct {
     int32_t out_packed;        /* BSMR_OUT_PACKED: unstaged row-block layouts carry each entry's CSR
                                   position in its metadata word (one 4-byte load per entry instead
                                   of two), 0 never, else whenever nnz <= 2^22; -1 = auto */
+    int32_t sweep;             /* BSMR_SWEEP: range sweep of staged-output row-block layouts (the
+                                  XCD's workgroups walk its column ranges in step),
+                                  0 never, else where it applies; -1 = auto */
+    int32_t sweep_range_kb;    /* BSMR_SWEEP_RANGE_KB: B bytes per sweep column range; -1 = 2048 */
+    float sweep_split;         /* BSMR_SWEEP_SPLIT: largest sweep task as a multiple of the mean;
+                                  < 0 = 1.5 */
+    int32_t sweep_slack;       /* BSMR_SWEEP_SLACK: steps a workgroup may run ahead of its XCD's
+                                  slowest; -1 = 1 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -221,6 +229,8 @@ typedef struct {
     /* bit i set: row-block layout i (as rb_rows) uses original-order row blocks (banded patterns
      * whose reordering scatters the band) */
     uint32_t rb_orig_rows;
+    /* bit i set: row-block layout i runs as a range sweep (k_sddmm_rb_sweep, bsmr_tuning.sweep) */
+    uint32_t rb_sweep;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

@@ -36,6 +36,8 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->item_cap = -1.0f;
     t->item_sched = -1;
     t->out_packed = -1;
+    t->sweep = t->sweep_range_kb = t->sweep_slack = -1;
+    t->sweep_split = -1.0f;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -83,6 +85,10 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     getf("BSMR_ITEM_CAP", t->item_cap);
     get3("BSMR_ITEM_SCHED", t->item_sched);
     get3("BSMR_OUT_PACKED", t->out_packed);
+    get3("BSMR_SWEEP", t->sweep);
+    geti("BSMR_SWEEP_RANGE_KB", t->sweep_range_kb);
+    getf("BSMR_SWEEP_SPLIT", t->sweep_split);
+    geti("BSMR_SWEEP_SLACK", t->sweep_slack);
     return n;
 }
 
@@ -137,6 +143,10 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->item_cap >= 0) p.item_cap = t->item_cap;
         if (t->item_sched >= 0)
             p.item_cost_cuts = p.item_lpt = p.small_sparse_rb = t->item_sched != 0;
+        if (t->sweep >= 0) p.sweep_mode = t->sweep ? 1 : 0;
+        if (t->sweep_range_kb >= 0) p.sweep_range_kb = static_cast<u32>(std::max(64, t->sweep_range_kb));
+        if (t->sweep_split >= 0) p.sweep_split = std::max(0.25f, t->sweep_split);
+        if (t->sweep_slack >= 0) p.sweep_slack = static_cast<u32>(t->sweep_slack);
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -352,6 +362,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_tiles[i] = L.rowBytes ? L.nTilesKept : 0;
         s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
         if (L.rowBytes && L.orig) s->rb_orig_rows |= 1u << i;
+        if (L.rowBytes && L.sweep) s->rb_sweep |= 1u << i;
     }
     s->dense_sampled_tiles = p.dense.built ? p.dense.nonempty : 0;
     return BSMR_OK;

@@ -1598,8 +1598,14 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // that XCD's L2 by the items before it (graph matrices: B is gathered once per row block and
     // column run, from L2 instead of the Infinity Cache)
     constexpr u32 CM = (1u << 22) - 1;
+    // range sweep (sddmm.hip k_sddmm_rb_sweep): staged output over reordered rows of >= 256 bytes
+    // with no kept MFMA tile; the XCD's column share in ranges of sweep_range_kb (2 MiB, or the
+    // user's l2_range_kb), walked by all of the XCD's workgroups in step (BSMR_DIAG & 262144: off)
+    const bool sweepWanted = stagedWanted && !orig && hkept.empty() && rowBytes >= 256 && sweep_mode != 0 &&
+                             !(diag & 262144) && n > 0;
+    const u32 rangeKb = sweepWanted && !l2_range_user ? sweep_range_kb : l2Kb;
     const u32 m = std::max<u32>(1, static_cast<u32>(std::ceil(
-        static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(l2Kb) * 1024.0))));
+        static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(rangeKb) * 1024.0))));
     const u32 NCR = XCD_BUCKETS * m;
     std::vector<u32> cuts(NCR + 1, N);
     cuts[0] = 0;
@@ -1916,17 +1922,119 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             if (cb[b] > 2 * target)
                 std::fprintf(stderr, "[rb layout]   block %u cost %.0f split %d nu %u\n", b, cb[b], split[b], nu[b]);
     }
+    std::vector<uint4> items;
+    std::vector<u32> ends;
+    // range sweep: per XCD, W = perBucket persistent workgroups (one per CU). Every row block
+    // with entries in the XCD's share is a task (heavy blocks several tasks, each 1/h of every
+    // range's entries, so no task exceeds sweep_split x the mean); tasks go to rounds of W by
+    // descending cost, each round's tasks to the workgroups least loaded so far. A task stages
+    // its image once and walks the XCD's m ranges in order, one item per outCap results; its
+    // items carry the step r m + k (round r, range k) at which the workgroups of the XCD meet
+    // (sddmm.hip k_sddmm_rb_sweep: a bounded wait, locality only)
+    const bool sweep = sweepWanted && staged && m >= 2 && NT == 1024;
+    std::vector<u32> wgStart, itemStep;
+    u32 sweepSteps = 0;
+    if (sweep) {
+        const u32 W = perBucket;
+        // cost cuts of an entry range into h parts (entries + piece_weight per column-run start)
+        auto part_cuts = [&](u32 e0, u32 ne, u32 h) {
+            std::vector<u32> pc(h + 1, e0 + ne);
+            pc[0] = e0;
+            if (h > 1) {
+                double tot = 0;
+                u32 run = 0;
+                for (u32 e = e0; e < e0 + ne; ++e) {
+                    const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+                    run = start ? 1 : run + 1;
+                    tot += 1.0 + (start ? piece_weight : 0.0);
+                }
+                double acc = 0;
+                u32 k = 1;
+                run = 0;
+                for (u32 e = e0; e < e0 + ne && k < h; ++e) {
+                    const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
+                    run = start ? 1 : run + 1;
+                    while (k < h && acc >= tot * k / h) pc[k++] = e;
+                    acc += 1.0 + (start ? piece_weight : 0.0);
+                }
+            }
+            return pc;
+        };
+        wgStart.reserve(static_cast<size_t>(XCD_BUCKETS) * W + 1);
+        for (u32 x = 0; x < XCD_BUCKETS; ++x) {
+            struct Task {
+                u32 b, j, h;
+                double c;
+            };
+            std::vector<Task> tasks;
+            std::vector<double> tc(nRB, 0.0);
+            double tot = 0;
+            u32 nz = 0;
+            for (u32 b = 0; b < nRB; ++b) {
+                for (u32 k = 0; k < m; ++k) tc[b] += cost[static_cast<size_t>(b) * NCR + x * m + k];
+                tot += tc[b];
+                nz += tc[b] > 0;
+            }
+            const double mean = nz ? tot / nz : 0.0;
+            for (u32 b = 0; b < nRB; ++b) {
+                if (tc[b] <= 0) continue;
+                const u32 h = std::max<u32>(1, static_cast<u32>(std::ceil(tc[b] / (sweep_split * mean))));
+                for (u32 j = 0; j < h; ++j) tasks.push_back({b, j, h, tc[b] / h});
+            }
+            std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.c > b.c; });
+            const u32 R = static_cast<u32>((tasks.size() + W - 1) / W);
+            sweepSteps = std::max(sweepSteps, R * m);
+            std::vector<double> load(W, 0.0);
+            std::vector<std::vector<std::pair<u32, u32>>> prog(W);  // (round, task)
+            std::vector<u32> byLoad(W);
+            for (u32 r = 0; r < R; ++r) {
+                for (u32 w = 0; w < W; ++w) byLoad[w] = w;
+                std::stable_sort(byLoad.begin(), byLoad.end(), [&](u32 a, u32 b) { return load[a] < load[b]; });
+                for (u32 q = 0; q < W && r * W + q < tasks.size(); ++q) {
+                    const u32 t = r * W + q, w = byLoad[q];
+                    prog[w].push_back({r, t});
+                    load[w] += tasks[t].c;
+                }
+            }
+            for (u32 w = 0; w < W; ++w) {
+                wgStart.push_back(static_cast<u32>(items.size()));
+                for (const auto& [r, t] : prog[w]) {
+                    const Task& T = tasks[t];
+                    bool first = true;
+                    for (u32 k = 0; k < m; ++k) {
+                        const size_t i = static_cast<size_t>(T.b) * NCR + x * m + k;
+                        const u32 ne = se1[i] - se0[i];
+                        if (!ne) continue;
+                        const std::vector<u32> pc = part_cuts(se0[i], ne, T.h);
+                        const u32 a0 = pc[T.j], a1 = pc[T.j + 1], len = a1 - a0;
+                        if (!len) continue;
+                        const u32 parts = (len + outCap - 1) / outCap;
+                        for (u32 q = 0; q < parts; ++q) {
+                            const u32 ea = a0 + static_cast<u32>(static_cast<u64>(len) * q / parts);
+                            const u32 eb = a0 + static_cast<u32>(static_cast<u64>(len) * (q + 1) / parts);
+                            items.push_back(make_uint4(T.b, 0, 0, ea));
+                            ends.push_back(eb);
+                            itemStep.push_back(((r * m + k) << 1) | (first ? 1u : 0u));
+                            first = false;
+                        }
+                    }
+                }
+            }
+        }
+        wgStart.push_back(static_cast<u32>(items.size()));
+    } else {
     size_t nmax = 0;
     for (const auto& l : lists) nmax = std::max(nmax, l.size());
     // staged layouts: an even number of list positions, so the launch can pair them (k_sddmm_rb)
     if (staged) nmax = (nmax + 1) & ~static_cast<size_t>(1);
-    std::vector<uint4> items(nmax * XCD_BUCKETS, make_uint4(0, 0, 0, 0));
-    std::vector<u32> ends(nmax * XCD_BUCKETS, 0);
+    items.assign(nmax * XCD_BUCKETS, make_uint4(0, 0, 0, 0));
+    ends.assign(nmax * XCD_BUCKETS, 0);
     for (u32 x = 0; x < XCD_BUCKETS; ++x)
         for (size_t j = 0; j < lists[x].size(); ++j) {
             items[j * XCD_BUCKETS + x] = lists[x][j];
             ends[j * XCD_BUCKETS + x] = lends[x][j];
         }
+    }
     // column-run pieces: each item's entries [e0, e1) cut at column changes and every
     // piece_max (<= RB_PIECE_MAX) entries; piece {first entry, column | (length - 1) << 22}. A workgroup's NG
     // row-groups take one piece each per phase, so phase ph runs the item's pieces
@@ -2065,6 +2173,19 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_HIP(hipStreamSynchronize(s));
         L.out.release();
         L.outPacked = true;
+    }
+    // the sweep kernel stores by runs only; without a run table the items (independent, in any
+    // order) run on k_sddmm_rb, one workgroup each
+    L.sweep = sweep && L.outRuns;
+    L.sweepW = L.sweep ? perBucket : 0;
+    L.sweepSteps = L.sweep ? sweepSteps : 0;
+    L.wgStart.release();
+    L.itemStep.release();
+    L.sweepDone.release();
+    if (L.sweep) {
+        BSMR_CHECK(L.wgStart.upload(wgStart.data(), wgStart.size(), s));
+        BSMR_CHECK(L.itemStep.upload(itemStep.data(), std::max<size_t>(itemStep.size(), 1), s));
+        BSMR_CHECK(L.sweepDone.alloc(static_cast<size_t>(XCD_BUCKETS) * std::max<u32>(sweepSteps, 1)));
     }
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
     BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));

@@ -88,6 +88,12 @@ struct Plan {
     double item_cap = -1.0;  // < 0: auto (build_rowblock_layout), 0: no cap
     bool item_cost_cuts = true, item_lpt = true;
     double item_fixed = 1024.0;
+    // range sweep of staged layouts (k_sddmm_rb_sweep): 0 off, else on; B bytes per range; the
+    // largest task as a multiple of the mean task cost; steps a workgroup may run ahead
+    int sweep_mode = 1;
+    u32 sweep_range_kb = 2048;
+    double sweep_split = 1.5;
+    u32 sweep_slack = 1;
     // sparse-row patterns with fewer row blocks than slots: one block per workgroup slot
     bool small_sparse_rb = true;
     bool stage_nt_auto = false;
@@ -171,6 +177,12 @@ struct Plan {
         // per result, and sortedPos is released
         bool outRuns = false;
         DevBuf<uint2> runs, itemRuns;
+        // range sweep (k_sddmm_rb_sweep): workgroup p = x W + w runs items [wgStart[p],
+        // wgStart[p + 1]); itemStep[i] = step << 1 | first item of its task (stages the image);
+        // sweepDone: per XCD and step, the workgroups that have left the step (reset per launch)
+        bool sweep = false;
+        u32 sweepW = 0, sweepSteps = 0;
+        DevBuf<u32> wgStart, itemStep, sweepDone;
         DevBuf<uint4> items;
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}

@@ -426,6 +426,14 @@ struct RbArgs {
     const uint2* runs;
     const uint2* itemRuns;
     u32 pairs;  // 1: each workgroup runs list positions 2j and 2j + 1 of its XCD (see k_sddmm_rb)
+    // range sweep (RowBlockLayout::sweep, k_sddmm_rb_sweep): workgroup x W + w runs items
+    // [wgStart[x W + w], wgStart[x W + w + 1]); itemStep[i] = step << 1 | restage; sweepDone[x S + g]
+    // counts the workgroups of XCD x past step g (S = sweepSteps); a workgroup enters step g once
+    // sweepDone[x S + g - slack - 1] reached W, or after a bounded wait
+    const u32* wgStart;
+    const u32* itemStep;
+    u32* sweepDone;
+    u32 sweepW, sweepSteps, sweepSlack;
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
@@ -766,8 +774,9 @@ template <int DT, int RBY, int NT, int OM>
 __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx, const bool prestaged,
                                         const u32 next) {
     // OM (output mode): 0 = one store per entry (a.outLds == 0), 1 = staged output (slots in
-    // LDS, written per item in CSR order), 2 = staged output by runs in pairs (PAIR)
-    constexpr bool PAIR = OM == 2, STAGED = OM != 0;
+    // LDS, written per item in CSR order), 2 = staged output by runs in pairs (PAIR), 3 = staged
+    // output without kept tiles, trace or ablations (the range sweep, LEAN)
+    constexpr bool PAIR = OM == 2, STAGED = OM != 0, LEAN = OM >= 2;
     using Geo = RowGeom<RBY>;
     constexpr u32 G = Geo::G, NC = Geo::NC;  // lanes per entry, chunks per lane
     constexpr u32 NW = NT / 64;               // waves per workgroup
@@ -776,7 +785,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // the pair kernel (PAIR): staged output by runs, no kept MFMA tiles, late B loads, default
     // staging policy, no trace or ablations (launch_rb picks it only then): its two items fit
     // the SGPR budget without those paths
-    const unsigned long long t0 = PAIR ? 0ull : rtime(a.trace);
+    const unsigned long long t0 = LEAN ? 0ull : rtime(a.trace);
     uint4 it = a.items[idx];
     // all four fields in SGPRs before the padding test: the compiler otherwise loads .x (the row
     // block) in a second, dependent round trip after the test
@@ -803,11 +812,15 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
         same_rb = nt.x == it.x;
     }
     const u32 q0 = a.qbase + it.x * a.RB;
-    const u32 tid = threadIdx.x, w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
+    u32 tid = threadIdx.x;
+    // LEAN (a loop of items per workgroup): the thread-derived values are recomputed per item
+    // rather than hoisted out of the caller's loop, where they would hold VGPRs across it
+    if constexpr (LEAN) asm volatile("" : "+v"(tid));
+    const u32 w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
     // every wave takes (at most) one dense tile and its row-groups one residual piece each per
     // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
     // staging loads so all of it is in flight together
-    const u32 ntile = !PAIR && (a.mode & 1) ? it.z - it.y : 0u;
+    const u32 ntile = !LEAN && (a.mode & 1) ? it.z - it.y : 0u;
     const u32 np = (a.mode & 2) ? pend - it.w : 0u;
     const u32 gr = tid / G;
     u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
@@ -833,7 +846,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     const u32 ws = __builtin_amdgcn_readfirstlane(w);  // wave index in an SGPR
     // the staging row indices are loaded first: they depend only on the item, so their round
     // trip overlaps the piece descriptor's, and the LDS-DMAs need not wait for the B columns
-    u32 rowv = a.row0;
+    u32 rowv = 0;  // (set before every staging: rb_stage_rows, or the pair's next rows)
     u32 src[ROWV ? 1 : MAXB];
     if (!prestaged) {
         if constexpr (ROWV) {
@@ -857,7 +870,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     const u32 tw = NW - 1 - w;
     Piece<RBY> pc;
     pc.len = 0;
-    if constexpr (!PAIR)
+    if constexpr (!LEAN)
         if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
     if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
     // staged output by runs: this lane's run descriptor (run w + NW * lane of the item), loaded
@@ -899,7 +912,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
         }
     };
     if (!prestaged) {
-        if (!PAIR && a.stageNt)
+        if (!LEAN && a.stageNt)  // (LEAN: the launch takes the default policy)
             stage(std::integral_constant<int, 2>{});
         else
             stage(std::integral_constant<int, 0>{});
@@ -907,7 +920,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // the phase-0 B columns and entry metadata: issued right behind the LDS-DMAs (so the
     // barrier's wait covers them too), or with lateB after the barrier (the barrier then waits
     // for the staging alone and the waves pay one load round trip before their first piece)
-    if (!PAIR && !a.lateB) {
+    if (!LEAN && !a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
         if (tw < ntile) dt.loadB(a, 0, tb);
     }
@@ -916,19 +929,19 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // not left to the compiler's wait insertion at the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (PAIR || a.lateB) {
+    if (LEAN || a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
-        if constexpr (!PAIR)
+        if constexpr (!LEAN)
             if (tw < ntile) dt.loadB(a, 0, tb);
     }
-    const unsigned long long tm = PAIR ? 0ull : rtime(a.trace);
-    if (!PAIR && (a.diag & 8)) {  // staging only
+    const unsigned long long tm = LEAN ? 0ull : rtime(a.trace);
+    if (!LEAN && (a.diag & 8)) {  // staging only
         trace_wave(a.trace, idx * NW + w, t0, tm);
         return false;
     }
-    if constexpr (!PAIR)
+    if constexpr (!LEAN)
         if (tw < ntile) dt.run(a, As, tb);
-    const unsigned long long td = PAIR ? 0ull : rtime(a.trace);
+    const unsigned long long td = LEAN ? 0ull : rtime(a.trace);
     // later phases (items with more pieces than row-groups, e.g. short column runs): phase ph
     // runs the column window [ph NG, (ph + 1) NG) of the item's pieces (longest first inside;
     // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
@@ -953,7 +966,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // (behind the pieces, not in their last phase: live across the phase loop, the descriptors
     // cost the loop VGPRs; a wave that ends early has them back before the store-pass barrier)
     if constexpr (STAGED) load_runs();
-    if constexpr (!PAIR) {
+    if constexpr (!LEAN) {
         for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
             dt.load(a, a.tileIds[t], q0, tb);
             dt.run(a, As, tb);
@@ -990,8 +1003,8 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
                 return true;
             }
         }
-        if (PAIR || !(a.diag & 128)) {  // (BSMR_DIAG & 128, ablation only: no P stores)
-            if (PAIR || a.runs) {
+        if (LEAN || !(a.diag & 128)) {  // (BSMR_DIAG & 128, ablation only: no P stores)
+            if (LEAN || a.runs) {
                 // wave w writes runs w, w + NW, ...: one contiguous store of up to 64 results
                 // per run (a row's results in this item, when rows are column-sorted), four
                 // runs per step with their LDS reads in flight together
@@ -1011,7 +1024,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
                     for (u32 u = 0; u < 4; ++u)  // (runs are at most 64 long)
                         if (lane < len[u]) a.P[pos[u] + lane] = v[u];
                 }
-            } else if constexpr (!PAIR) {
+            } else if constexpr (!LEAN) {
                 // eight position loads in flight per lane before their stores: a loop of
                 // dependent load -> store pairs exposed one L2 latency per 1024 results (C4 x0.5:
                 // 1.135 -> 1.082 ms). Issuing the first batch before the barrier measured slower
@@ -1042,7 +1055,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
             }
         }
     }
-    if constexpr (!PAIR) trace_wave(a.trace, idx * NW + w, t0, tm, td);
+    if constexpr (!LEAN) trace_wave(a.trace, idx * NW + w, t0, tm, td);
     return staged_next;
 }
 
@@ -1308,9 +1321,67 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
         rb_item<DT, RBY, NT, 2>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
 }
 
+// the longest a workgroup waits for its XCD's slowest workgroup to leave a step (s_memrealtime
+// ticks, 100 MHz): the wait only keeps the XCD's workgroups inside a window of column ranges (B
+// lines shared in L2); past it the workgroup goes on, so no step ever depends on co-residency
+constexpr u32 SWEEP_WAIT_TICKS = 3000;  // 30 us
+
+// Range sweep (staged output, Plan::build_rowblock_layout): the XCD's W workgroups (one per CU)
+// each run a list of tasks; a task stages its row block's image once and walks the XCD's column
+// ranges in order, one item per staged-output load. Entering a later step, a workgroup counts
+// itself out of the steps before it and waits (bounded) until every workgroup of its XCD has
+// left step g - slack - 1, so the XCD's L2 holds the B columns of at most slack + 1 ranges at a
+// time instead of every range the XCD's items happen to be in
+// the workgroup leaves steps [from, to) of its XCD, then waits (bounded) until every workgroup
+// of the XCD has left step to - slack - 1 (thread 0; the caller's barrier holds the others)
+__device__ __forceinline__ void sweep_leave(const RbArgs& a, const u32 from, const u32 to) {
+    if (threadIdx.x != 0) return;
+    // (the counters' address is recomputed here: fewer SGPRs live across the items)
+    u32* done = a.sweepDone + static_cast<size_t>(blockIdx.x % XCD_BUCKETS) * a.sweepSteps;
+    for (u32 k = from; k < to; ++k)
+        __hip_atomic_fetch_add(done + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (to < a.sweepSteps && to > a.sweepSlack) {
+        const u32* gate = done + (to - a.sweepSlack - 1);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.sweepW &&
+               __builtin_amdgcn_s_memrealtime() - t0 < SWEEP_WAIT_TICKS)
+            __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <int DT, int RBY, int NT>
+__global__ __launch_bounds__(NT, 4) void k_sddmm_rb_sweep(RbArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char AsB[];
+    char* As = AsB;
+    if (blockIdx.y) {  // batch b (its workgroups share the counters: they then only gate earlier)
+        a.A += blockIdx.y * a.bA;
+        a.B += blockIdx.y * a.bB;
+        a.P += blockIdx.y * a.bP;
+    }
+    const u32 pw = (blockIdx.x % XCD_BUCKETS) * a.sweepW + blockIdx.x / XCD_BUCKETS;
+    const u32 i1 = __builtin_amdgcn_readfirstlane(a.wgStart[pw + 1]);
+    u32 g = 0;  // the workgroup's step: it has counted itself out of every step before it
+    for (u32 i = __builtin_amdgcn_readfirstlane(a.wgStart[pw]); i < i1; ++i) {
+        const u32 st = __builtin_amdgcn_readfirstlane(a.itemStep[i]);
+        const u32 step = st >> 1;
+        const bool restage = (st & 1) != 0;
+        if (step > g) {
+            __syncthreads();  // the previous item is done (its slots and image read)
+            sweep_leave(a, g, step);  // and (bounded) wait until the XCD has left step - slack - 1
+            g = step;
+            __syncthreads();
+        } else if (restage) {
+            __syncthreads();  // no wave still reads the previous image or its slots
+        }
+        rb_item<DT, RBY, NT, 3>(a, As, i, !restage, NO_ITEM);
+    }
+    sweep_leave(a, g, a.sweepSteps);
+}
+
 template <int DT, int RBY>
-void (*pick_rb(const u32 NT, const bool pairs))(RbArgs) {
+void (*pick_rb(const u32 NT, const bool pairs, const bool sweep))(RbArgs) {
     if constexpr (RBY >= 256) {  // (no pairs at 128-byte rows: launch_rb enables them from 256)
+        if (sweep && NT == 1024) return k_sddmm_rb_sweep<DT, RBY, 1024>;
         if (pairs) return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024> : k_sddmm_rb_pair<DT, RBY, 512>;
     }
     return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>;
@@ -1458,6 +1529,16 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
                       !(p.diag & (8u | 32u | 64u | 128u | 16384u))
                   ? 1u
                   : 0u;
+    if (L.sweep) {
+        a.pairs = 0;
+        a.wgStart = L.wgStart.data();
+        a.itemStep = L.itemStep.data();
+        a.sweepDone = L.sweepDone.data();
+        a.sweepW = L.sweepW;
+        a.sweepSteps = L.sweepSteps;
+        a.sweepSlack = p.sweep_slack;
+        BSMR_HIP(hipMemsetAsync(L.sweepDone.data(), 0, static_cast<size_t>(XCD_BUCKETS) * L.sweepSteps * 4, s));
+    }
     a.tilePanel = p.denseItems.data();
     a.tileIds = L.tileIds.data();
     a.denseCols = p.denseCols.data();
@@ -1472,7 +1553,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0)
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, L.sweep)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
@@ -1487,7 +1568,8 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
 #undef BSMR_RB2
 #undef BSMR_RB
     // k_sddmm_rb stages a fixed 160 / 80 KiB per workgroup (the image and an unused tail)
-    hipLaunchKernelGGL(fn, dim3(a.pairs ? L.nItems / 2 : L.nItems, nb), dim3(L.NT),
+    const u32 grid = L.sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
+    hipLaunchKernelGGL(fn, dim3(grid, nb), dim3(L.NT),
                        (L.NT == 1024 ? 160 : 80) * 1024, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
