@@ -129,7 +129,8 @@ typedef struct {
                                   of two), 0 never, else whenever nnz <= 2^22; -1 = auto */
     int32_t sweep;             /* BSMR_SWEEP: range sweep of staged-output row-block layouts (the
                                   XCD's workgroups walk its column ranges in step),
-                                  0 never, else where it applies; -1 = auto */
+                                  0 never, else where it applies; -1 = auto = never (C4 x1
+                                  4.6 vs 3.7 ms) */
     int32_t sweep_range_kb;    /* BSMR_SWEEP_RANGE_KB: B bytes per sweep column range; -1 = 2048 */
     float sweep_split;         /* BSMR_SWEEP_SPLIT: largest sweep task as a multiple of the mean;
                                   < 0 = 1.5 */

@@ -90,7 +90,7 @@ struct Plan {
     double item_fixed = 1024.0;
     // range sweep of staged layouts (k_sddmm_rb_sweep): 0 off, else on; B bytes per range; the
     // largest task as a multiple of the mean task cost; steps a workgroup may run ahead
-    int sweep_mode = 1;
+    int sweep_mode = 0;  // off by default: C4 x1 4.61 vs 3.72 ms (profiles/r04v, r04w)
     u32 sweep_range_kb = 2048;
     double sweep_split = 1.5;
     u32 sweep_slack = 1;
