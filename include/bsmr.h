@@ -22,11 +22,12 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 8  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 9  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
                               the plan options (no environment reads in the library);
-                              7: bsmr_tuning.out_packed; 8: bsmr_tuning.sweep*, rb_sweep */
+                              7: bsmr_tuning.out_packed; 8: bsmr_tuning.sweep*, rb_sweep;
+                              9: bsmr_tuning.cluster_filter, filter stats */
 
 typedef enum {
     BSMR_OK = 0,
@@ -136,6 +137,11 @@ typedef struct {
                                   < 0 = 1.5 */
     int32_t sweep_slack;       /* BSMR_SWEEP_SLACK: steps a workgroup may run ahead of its XCD's
                                   slowest; -1 = 1 */
+    int32_t cluster_filter;    /* BSMR_CLUSTER_FILTER: bound every pair's similarity on the matrix
+                                  cores before the clustering chain and skip the pairs that cannot
+                                  reach alpha (same permutation), 0 never, 1 when
+                                  alpha >= 0.01 and its buffers fit a quarter of the free memory,
+                                  -1 = auto (the same, from 32768 rows) */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -232,6 +238,10 @@ typedef struct {
     uint32_t rb_orig_rows;
     /* bit i set: row-block layout i runs as a range sweep (k_sddmm_rb_sweep, bsmr_tuning.sweep) */
     uint32_t rb_sweep;
+    /* clustering candidate filter (bsmr_tuning.cluster_filter): 1 when it ran, and its time
+     * (included in row_reorder_ms) */
+    uint32_t cluster_filter_used;
+    float cluster_filter_ms;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

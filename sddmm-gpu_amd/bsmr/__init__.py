@@ -47,7 +47,8 @@ class Tuning(C.Structure):
                 ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32), ("seg_items", C.c_int32),
                 ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
                 ("item_sched", C.c_int32), ("out_packed", C.c_int32), ("sweep", C.c_int32),
-                ("sweep_range_kb", C.c_int32), ("sweep_split", C.c_float), ("sweep_slack", C.c_int32)]
+                ("sweep_range_kb", C.c_int32), ("sweep_split", C.c_float), ("sweep_slack", C.c_int32),
+                ("cluster_filter", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -79,7 +80,8 @@ class PlanStats(C.Structure):
                 ("rb_pieces", C.c_uint32 * 5), ("rb_entries", C.c_uint32 * 5),
                 ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5),
                 ("dense_sampled_tiles", C.c_uint32), ("rb_orig_rows", C.c_uint32),
-                ("rb_sweep", C.c_uint32)]
+                ("rb_sweep", C.c_uint32), ("cluster_filter_used", C.c_uint32),
+                ("cluster_filter_ms", C.c_float)]
 
     def as_dict(self):
         d = {}
@@ -119,7 +121,7 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 8  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 9  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -236,7 +238,7 @@ def tuning_from_env(env=None):
         v = env.get(TUNING_ENV[f])
         if v is None:
             continue
-        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "sweep"):  # tri-state: "0" never, "1" always, else auto
+        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "sweep", "cluster_filter"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
         elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap", "sweep_split"):
             out[f] = float(v)

@@ -38,6 +38,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->out_packed = -1;
     t->sweep = t->sweep_range_kb = t->sweep_slack = -1;
     t->sweep_split = -1.0f;
+    t->cluster_filter = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -89,6 +90,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     geti("BSMR_SWEEP_RANGE_KB", t->sweep_range_kb);
     getf("BSMR_SWEEP_SPLIT", t->sweep_split);
     geti("BSMR_SWEEP_SLACK", t->sweep_slack);
+    get3("BSMR_CLUSTER_FILTER", t->cluster_filter);
     return n;
 }
 
@@ -147,6 +149,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->sweep_range_kb >= 0) p.sweep_range_kb = static_cast<u32>(std::max(64, t->sweep_range_kb));
         if (t->sweep_split >= 0) p.sweep_split = std::max(0.25f, t->sweep_split);
         if (t->sweep_slack >= 0) p.sweep_slack = static_cast<u32>(t->sweep_slack);
+        if (t->cluster_filter >= 0) p.cluster_filter = t->cluster_filter ? 1 : 0;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -350,6 +353,8 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
     s->exact_similarity_evals = p.exact_evals;
     s->total_similarity_evals = p.total_evals;
     s->row_reorder_ms = p.row_ms;
+    s->cluster_filter_used = p.filter_used ? 1u : 0u;
+    s->cluster_filter_ms = p.filter_ms;
     s->col_reorder_ms = p.col_ms;
     s->dense_items = p.nDenseItems;
     s->residual_items = p.nResItems;

@@ -183,6 +183,10 @@ struct ClusterArgs {
     float alpha;
     int exact_all;
     u64 timeout_ticks;  // s_memrealtime ticks (100 MHz)
+    // candidate filter (cluster_filter.hip), or null: bit p of row q set when position p may
+    // join the cluster led by position q while it is that row alone; fW = words per full row
+    const u32* fbits;
+    u32 fW;
     // BSMR_DIAG & 2048: per tile (global index (first cluster - 1) / T) 16 u64: kernel entry,
     // start found, end (s_memrealtime), windows, empty windows, sub-batch rounds, evaluations,
     // ticket, ticks in window scans (spins included), in evaluation, in the leader's resolution,
@@ -225,6 +229,10 @@ struct ClusterCtl {
     u64 S1R[CL_TMAX];      // kept-block sum of the representative
     u32 scanL[CL_WIN / 64], scanN[CL_WIN / 64];  // window scan: ready prefix, unassigned count
     u32 ntodo, t, nact, done, i, nact_eval;
+    u32 lead[CL_TMAX];  // position that started each tile cluster (candidate filter)
+    u32 multi;          // bit c: cluster c holds more than its leader row (the filter cannot skip it)
+    u32 nev;            // rows of the sub-batch the filter keeps, in evl (position order)
+    u32 evl[CL_WIN];
     u32 nxt;  // the sub-batch's next row for a free wave (rows t .. t + 15 go to waves 0 .. 15)
     u64 nexact, ntotal;
     u64 tr_begin, tr_started;  // BSMR_DIAG & 2048 timeline (ClusterArgs::ctrace)
@@ -487,7 +495,9 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
         C.tr_scan = C.tr_eval = C.tr_lead = C.tr_own = C.tr_ent = 0;
         C.tr_win = C.tr_idle = C.tr_sub = 0;
     }
+    if (tid == 0) C.multi = 0;
     if (tid < CL_TMAX) {
+        C.lead[tid] = 0;
         C.inrf[tid] = 0.0f;
         C.nr[tid] = 0.0f;
         C.SR[tid] = 0;
@@ -527,6 +537,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
         if (l == 0) {
             set_norm(c, m.z);
             C.S1R[c] = m.w;
+            C.lead[c] = p;
             C.nact = c + 1;
             st_agent(&a.state[p], ASSIGNED | (kfirst + c));
             st_agent(&a.st[kfirst + c], p + 2);
@@ -550,6 +561,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
         if (l == 0) {
             set_norm(c, C.SR[c] + dsr);
             C.S1R[c] += ds1;
+            C.multi |= 1u << c;
             st_agent(&a.state[p], ASSIGNED | (kfirst + c));
         }
     };
@@ -714,33 +726,81 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 ++C.tr_sub;
                 if (a.ctrace) C.tr_t0 = now_ticks();
             }
-            const u32 tend = min(ntodo, t + CL_SUB);
+            // with the candidate filter a sub-batch is the whole window (skipped rows cost a bit
+            // test, not an evaluation)
+            const u32 tend = min(ntodo, t + (a.fbits ? CL_WIN : CL_SUB));
+            u32 nev = tend - t;
+            if (a.fbits) {
+                // a row needs its evaluation only if some tile cluster holds more than its leader
+                // row, or the bound of (leader, row) may reach alpha; the others are rejected by
+                // every tile cluster (res 0). Each wave tests its rows' words in one round trip.
+                constexpr u32 FR = CL_WIN / CL_WAVES;
+                const u32 multi = C.multi;
+                const u32 q = l < nact ? C.lead[l] : 0u;
+                const u64 qo = fbits_row_offset(q, a.fW);
+                u32 word[FR];
+#pragma unroll
+                for (u32 k = 0; k < FR; ++k) {
+                    const u32 j = t + w + CL_WAVES * k;
+                    const u32 p = j < tend ? C.todo[j] : 0u;
+                    const bool look = j < tend && l < nact && !((multi >> l) & 1u) && p > q;
+                    word[k] = look ? a.fbits[qo + (p >> 5) - (q >> 5)] : ~0u;
+                }
+#pragma unroll
+                for (u32 k = 0; k < FR; ++k) {
+                    const u32 j = t + w + CL_WAVES * k;
+                    const u32 p = j < tend ? C.todo[j] : 0u;
+                    const u64 b = __ballot(l < nact && ((word[k] >> (p & 31)) & 1u));
+                    if (l == 0 && j < tend) C.res[j] = b != 0 ? 1u : 0u;
+                }
+                __syncthreads();
+                if (w == 0) {
+                    u32 n = 0;
+                    for (u32 j0 = t; j0 < tend; j0 += 64) {
+                        const u32 j = j0 + l;
+                        const bool need = j < tend && C.res[j] != 0;
+                        const u64 b = __ballot(need);
+                        if (need)
+                            C.evl[n + __builtin_amdgcn_mbcnt_hi(static_cast<u32>(b >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo(static_cast<u32>(b), 0u))] = j;
+                        n += static_cast<u32>(__builtin_popcountll(b));
+                    }
+                    if (l == 0) {
+                        C.nev = n;
+                        C.nxt = t + CL_WAVES;
+                    }
+                }
+                __syncthreads();
+                nev = C.nev;
+            }
             {
-                u32 j = t + w;
+                // row k of the sub-batch's evaluation list (whichever wave is free takes the next)
+                auto row_at = [&](u32 k) { return a.fbits ? C.evl[k] : t + k; };
+                u32 k = w;
                 u32 pre[4];
                 uint4 m = make_uint4(0, 0, 0, 0);
-                if (j < tend) {
-                    m = C.meta[j];
+                if (k < nev) {
+                    m = C.meta[row_at(k)];
                     load_chunk0(a, m, pre);
                 }
-                while (j < tend) {
+                while (k < nev) {
                     // the next row comes from the sub-batch's counter: rows go to whichever wave
                     // is free, so a long row no longer holds a fixed three others behind it
                     // (wave 0 spent 40 % of the evaluation phase waiting at the barrier on
                     // reddit-like x1; profiles/r03j/cltrace)
-                    u32 jn = 0;
-                    if (l == 0) jn = atomicAdd(&C.nxt, 1u);
-                    jn = __builtin_amdgcn_readfirstlane(jn);
+                    u32 kn = 0;
+                    if (l == 0) kn = atomicAdd(&C.nxt, 1u) - t;
+                    kn = __builtin_amdgcn_readfirstlane(kn);
                     const u32 cur[4] = {pre[0], pre[1], pre[2], pre[3]};
                     const uint4 mc = m;
-                    if (jn < tend) {  // the next row's first chunk in flight while this one runs
-                        m = C.meta[jn];
+                    if (kn < nev) {  // the next row's first chunk in flight while this one runs
+                        m = C.meta[row_at(kn)];
                         load_chunk0(a, m, pre);
                     }
                     const u32 r = eval_row<TS>(a, reps, C, mc, cur, nact);
-                    if (l == 0) C.res[j] = r;
+                    if (l == 0) C.res[row_at(k)] = r;
                     if (a.ctrace && tid == 0) C.tr_ent += mc.y;
-                    j = jn;
+                    k = kn;
                 }
             }
             if (a.ctrace && tid == 0) C.tr_own += now_ticks() - C.tr_t0;  // wave 0's own rows
@@ -2267,7 +2327,35 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     hipLaunchKernelGGL(k_pmeta, dim3(grid_for(M, 256)), dim3(256), 0, s, asc.data(), rowptr.data(),
                        nblk.data(), SC.data(), S1C.data(), M, pmeta.data());
     BSMR_HIP(hipGetLastError());
+    // candidate filter: an MFMA pass over every pair of rows bounds their similarity, so the
+    // chain skips the pairs that cannot reach alpha (cluster_filter.hip)
+    DevBuf<u32> fbits;
+    u32 fW = 0;
+    filter_used = false;
+    filter_ms = 0.f;
+    if (cluster_filter != 0 && !exact_all && alpha >= 0.01f && M - z >= 2 &&
+        (cluster_filter == 1 || M >= filter_min_rows)) {
+        size_t fr = 0, tot = 0;
+        BSMR_HIP(hipMemGetInfo(&fr, &tot));
+        const u64 Kp = (nbpr + 63ull) / 64 * 64;
+        const u64 need = static_cast<u64>(M) * Kp * 2 + sim_filter_words(M) * 4 + static_cast<u64>(M) * 8;
+        if (need <= fr / 4) {
+            hipEvent_t f0, f1;
+            BSMR_HIP(hipEventCreate(&f0));
+            BSMR_HIP(hipEventCreate(&f1));
+            BSMR_HIP(hipEventRecord(f0, s));
+            BSMR_CHECK(build_sim_filter(pmeta.data(), enc.data(), M, nbpr, B, keptMask, alpha, fbits, fW, s));
+            BSMR_HIP(hipEventRecord(f1, s));
+            BSMR_HIP(hipEventSynchronize(f1));
+            BSMR_HIP(hipEventElapsedTime(&filter_ms, f0, f1));
+            BSMR_HIP(hipEventDestroy(f0));
+            BSMR_HIP(hipEventDestroy(f1));
+            filter_used = true;
+        }
+    }
     ClusterArgs ca{};
+    ca.fbits = filter_used ? fbits.data() : nullptr;
+    ca.fW = fW;
     ca.pmeta = pmeta.data();
     ca.enc = enc.data();
     ca.state = state.data();

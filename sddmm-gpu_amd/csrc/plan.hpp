@@ -24,6 +24,12 @@ int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype,
 int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
                  hipStream_t s, u32 nb = 1);
 
+// clustering candidate filter (cluster_filter.hip): the bit triangle of pairs (leader q,
+// position p > q) whose similarity bound may reach alpha; W = words per full row
+int build_sim_filter(const uint4* pmeta, const u32* enc, u32 M, u32 nbpr, u32 B, u32 keptMask, float alpha,
+                     DevBuf<u32>& bits, u32& W, hipStream_t s);
+u64 sim_filter_words(u32 M);
+
 u32 block_size_for(u32 M, u32 N, u64 free_mem);
 u32 cluster_block_dim(u32 nbpr);
 u32 kept_warp_mask(u32 B);
@@ -105,6 +111,13 @@ struct Plan {
     // clusters per persistent clustering launch (bsmr_plan_options.cluster_batch); r01k timing
     // on reddit_like x0.25: 512 -> 9.7 s, 4096 -> 4.6 s, 16384 -> 2.3 s (fewer host round trips, more in flight)
     u32 cluster_batch = 16384;
+    // clustering candidate filter (cluster_filter.hip; bsmr_tuning.cluster_filter): -1 auto (M >=
+    // filter_min_rows, alpha >= 0.01, the filter's buffers fit a quarter of the free memory), 0
+    // never, 1 whenever alpha >= 0.01 and it fits
+    int cluster_filter = -1;
+    u32 filter_min_rows = 32768;
+    bool filter_used = false;
+    float filter_ms = 0.f;
 
     // input
     DevBuf<u32> rowptr, colidx;

@@ -26,6 +26,13 @@ __device__ __forceinline__ void st_agent(u32* p, u32 v) {
 
 __device__ __forceinline__ u32 lane_id() { return __lane_id(); }
 
+// clustering candidate filter (cluster_filter.hip): row q of the bit triangle holds the 32-bit
+// words [q / 32, W) of positions p, so it starts at sum_{r < q} (W - r / 32)
+__host__ __device__ __forceinline__ u64 fbits_row_offset(u32 q, u32 W) {
+    const u64 a = q >> 5, b = q & 31;
+    return static_cast<u64>(q) * W - (16 * a * (a - 1) + a * b);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

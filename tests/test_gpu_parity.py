@@ -109,6 +109,57 @@ def nips_like_case():
     return synth.nips_like()
 
 
+@pytest.mark.parametrize("name", ["ragged_empty_rows", "zipf", "wide_bs20", "blocky",
+                                  "trefethen_small", "mycielskian10"])
+@pytest.mark.parametrize("alpha", [0.1, 0.3, 0.9])
+def test_cluster_filter_same_permutation(name, alpha):
+    """The clustering's candidate filter (cluster_filter.hip: an MFMA bound of every pair's
+    similarity, pairs that cannot reach alpha skipped by the chain) forced on: the permutation and
+    cluster count equal the oracle's first-fit (rowReordering.cu:325-432, 893-1007), and the
+    chain walks the same number of (position, cluster) pairs as without the filter."""
+    M, N, rp, ci = small_cases()[name]
+    on = Plan(M, N, rp, ci, alpha=alpha, delta=0.3, free_mem_bytes=FREE,
+              tuning=tuning_from_env({"BSMR_CLUSTER_FILTER": "1"}))
+    off = Plan(M, N, rp, ci, alpha=alpha, delta=0.3, free_mem_bytes=FREE,
+               tuning=tuning_from_env({"BSMR_CLUSTER_FILTER": "0"}))
+    s_on, s_off = on.stats(), off.stats()
+    assert s_on["cluster_filter_used"] == 1 and s_off["cluster_filter_used"] == 0
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    rows, ncl, _ = O.row_reorder(c, np.float32(alpha), O.block_size(M, N, FREE))
+    assert s_on["num_clusters"] == ncl
+    assert np.array_equal(on.array("reorderedRows"), rows)
+    assert s_on["total_similarity_evals"] == s_off["total_similarity_evals"]
+    assert s_on["exact_similarity_evals"] == s_off["exact_similarity_evals"]
+
+
+@pytest.mark.parametrize("scale,alpha", [(0.02, 0.3), (0.05, 0.3), (0.05, 0.1), (0.05, 0.7)])
+def test_cluster_filter_reddit_like(scale, alpha):
+    """A power-law graph (almost every position starts its own cluster, so the chain compares
+    nearly all pairs): the filtered chain gives the same permutation as the unfiltered one."""
+    M, N, rp, ci = synth.reddit_like(scale)
+    perms, stats = [], []
+    for f in ("1", "0"):
+        plan = Plan(M, N, rp, ci, alpha=alpha, delta=0.3, free_mem_bytes=FREE,
+                    tuning=tuning_from_env({"BSMR_CLUSTER_FILTER": f}))
+        perms.append(plan.array("reorderedRows"))
+        stats.append(plan.stats())
+    assert stats[0]["cluster_filter_used"] == 1
+    assert stats[0]["num_clusters"] == stats[1]["num_clusters"]
+    assert np.array_equal(perms[0], perms[1])
+    assert stats[0]["total_similarity_evals"] == stats[1]["total_similarity_evals"]
+
+
+def test_cluster_filter_nips_like_bit_exact():
+    """nips-like (C1/C2's pattern) with the filter forced on: plan arrays equal the oracle's."""
+    M, N, rp, ci = nips_like_case()
+    gp = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,
+              tuning=tuning_from_env({"BSMR_CLUSTER_FILTER": "1"}))
+    assert gp.stats()["cluster_filter_used"] == 1
+    _, op, ncl = oracle_plan(M, N, rp, ci, 0.3, 0.3, FREE)
+    assert gp.stats()["num_clusters"] == ncl
+    assert_plans_equal(gp, op)
+
+
 def test_nips_like_plan_bit_exact():
     M, N, rp, ci = nips_like_case()
     gp = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Build gate: parse hipcc's -Rpass-analysis=kernel-resource-usage remarks and fail when an SDDMM
-kernel (k_sddmm*) spills VGPRs/SGPRs or uses scratch. Usage: check_kernel_resources.py <remarks>"""
+kernel (k_sddmm*, k_sim_filter) spills VGPRs/SGPRs or uses scratch. Usage: check_kernel_resources.py <remarks>"""
 import os
 import re
 import sys
@@ -13,9 +13,9 @@ def main(path):
             m = re.search(r"remark:\s+Function Name: (\S+)", line)
             if m:
                 kern = m.group(1)
-                seen += "k_sddmm" in kern
+                seen += "k_sddmm" in kern or "k_sim_filter" in kern
                 continue
-            if not kern or "k_sddmm" not in kern:
+            if not kern or ("k_sddmm" not in kern and "k_sim_filter" not in kern):
                 continue
             allow = os.environ.get("RES_CHECK_ALLOW")  # experiments only: a regex of kernels
             if allow and re.search(allow, kern):
@@ -28,7 +28,7 @@ def main(path):
         sys.stderr.write("kernel resource check failed (spills/scratch):\n  " + "\n  ".join(bad) + "\n")
         return 1
     if seen == 0:
-        sys.stderr.write(f"kernel resource check: no k_sddmm kernels in {path}\n")
+        sys.stderr.write(f"kernel resource check: no k_sddmm / k_sim_filter kernels in {path}\n")
         return 1
     return 0
 

@@ -46,6 +46,9 @@ def main():
                           "col_reorder_ms": round(st["col_reorder_ms"], 2),
                           "num_clusters": st["num_clusters"],
                           "total_similarity_evals": st["total_similarity_evals"],
+                          "exact_similarity_evals": st["exact_similarity_evals"],
+                          "cluster_filter_used": st["cluster_filter_used"],
+                          "cluster_filter_ms": round(st["cluster_filter_ms"], 2),
                           "same_permutation_as_first": same}
         print(json.dumps({b: out["runs"][b]}), file=sys.stderr, flush=True)
         del plan
