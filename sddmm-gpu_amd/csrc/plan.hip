@@ -190,7 +190,8 @@ struct ClusterArgs {
     // BSMR_DIAG & 2048: per tile (global index (first cluster - 1) / T) 16 u64: kernel entry,
     // start found, end (s_memrealtime), windows, empty windows, sub-batch rounds, evaluations,
     // ticket, ticks in window scans (spins included), in evaluation, in the leader's resolution,
-    // exact evaluations, ticks wave 0 spent on its own rows, encoding entries wave 0 read; else
+    // exact evaluations, ticks wave 0 spent on its own rows, encoding entries wave 0 read, rows
+    // evaluated (the candidate filter's survivors), clusters holding more than their leader; else
     // null
     unsigned long long* ctrace;
 };
@@ -233,10 +234,14 @@ struct ClusterCtl {
     u32 multi;          // bit c: cluster c holds more than its leader row (the filter cannot skip it)
     u32 nev;            // rows of the sub-batch the filter keeps, in evl (position order)
     u32 evl[CL_WIN];
+    // the candidate bits of the window for each tile cluster: words wb0 .. wb0 + CL_WB - 1 of its
+    // leader's row (~0 where the row stores no word: positions before the leader)
+    u32 wb0;
+    u32 wbits[CL_TMAX][CL_WIN / 32 + 1];
     u32 nxt;  // the sub-batch's next row for a free wave (rows t .. t + 15 go to waves 0 .. 15)
     u64 nexact, ntotal;
     u64 tr_begin, tr_started;  // BSMR_DIAG & 2048 timeline (ClusterArgs::ctrace)
-    u64 tr_t0, tr_scan, tr_eval, tr_lead, tr_own, tr_ent;
+    u64 tr_t0, tr_scan, tr_eval, tr_lead, tr_own, tr_ent, tr_nev;
     u32 tr_win, tr_idle, tr_sub;
 };
 
@@ -492,10 +497,13 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
     if (tid == 0) {
         C.tr_begin = a.ctrace ? now_ticks() : 0ull;
         C.tr_started = 0;
-        C.tr_scan = C.tr_eval = C.tr_lead = C.tr_own = C.tr_ent = 0;
+        C.tr_scan = C.tr_eval = C.tr_lead = C.tr_own = C.tr_ent = C.tr_nev = 0;
         C.tr_win = C.tr_idle = C.tr_sub = 0;
     }
-    if (tid == 0) C.multi = 0;
+    if (tid == 0) {
+        C.multi = 0;
+        C.wb0 = 0;
+    }
     if (tid < CL_TMAX) {
         C.lead[tid] = 0;
         C.inrf[tid] = 0.0f;
@@ -527,9 +535,20 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
         C.nr[c] = nr;
         C.inrf[c] = sr ? 1.0f / nr : 0.0f;
     };
+    // candidate filter: lanes k < CL_WIN / 32 + 1 load the window's words of the row of leader q
+    // (cluster c) into LDS; wbit(c, p): may position p (in the window) join cluster c's leader
+    constexpr u32 CL_WB = CL_WIN / 32 + 1;
+    auto load_wbits = [&](u32 c, u32 q) {
+        if (l < CL_WB) {
+            const u32 wd = C.wb0 + l, qw = q >> 5;
+            C.wbits[c][l] = wd >= qw && wd < a.fW ? a.fbits[fbits_row_offset(q, a.fW) + (wd - qw)] : ~0u;
+        }
+    };
+    auto wbit = [&](u32 c, u32 p) -> bool { return (C.wbits[c][(p >> 5) - C.wb0] >> (p & 31)) & 1u; };
     // leader: start a new tile cluster (index C.nact) at position p (metadata m)
     auto new_cluster = [&](u32 p, uint4 m) {
         const u32 c = C.nact;
+        if (a.fbits) load_wbits(c, p);
         for (u32 e = l; e < m.y; e += 64) {
             const u32 ent = a.enc[m.x + e];
             reps[(ent & 0xFFFFu) * TS + c] = ent >> 16;
@@ -708,6 +727,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 C.t = 0;
                 C.nxt = CL_WAVES;
                 C.i = i + total;
+                C.wb0 = i >> 5;
                 if (aborted) {
                     C.done = 1;
                     C.nact = T;
@@ -716,6 +736,16 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
             }
         }
         __syncthreads();
+        if (a.fbits && w == 0) {
+            // the window's candidate bits of every tile cluster (x = CL_WB c + k; T = 8 takes two
+            // passes of the wave)
+            const u32 na = C.nact;
+            for (u32 x = l; x < na * CL_WB; x += 64) {
+                const u32 c = x / CL_WB, k = x - c * CL_WB;
+                const u32 q = C.lead[c], wd = C.wb0 + k, qw = q >> 5;
+                C.wbits[c][k] = wd >= qw && wd < a.fW ? a.fbits[fbits_row_offset(q, a.fW) + (wd - qw)] : ~0u;
+            }
+        }
         if (a.ctrace && tid == 0) C.tr_scan += now_ticks() - C.tr_t0;
         if (C.done && C.ntodo == 0) break;
         // ---- evaluate / resolve sub-batches
@@ -732,33 +762,19 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
             u32 nev = tend - t;
             if (a.fbits) {
                 // a row needs its evaluation only if some tile cluster holds more than its leader
-                // row, or the bound of (leader, row) may reach alpha; the others are rejected by
-                // every tile cluster (res 0). Each wave tests its rows' words in one round trip.
-                constexpr u32 FR = CL_WIN / CL_WAVES;
-                const u32 multi = C.multi;
-                const u32 q = l < nact ? C.lead[l] : 0u;
-                const u64 qo = fbits_row_offset(q, a.fW);
-                u32 word[FR];
-#pragma unroll
-                for (u32 k = 0; k < FR; ++k) {
-                    const u32 j = t + w + CL_WAVES * k;
-                    const u32 p = j < tend ? C.todo[j] : 0u;
-                    const bool look = j < tend && l < nact && !((multi >> l) & 1u) && p > q;
-                    word[k] = look ? a.fbits[qo + (p >> 5) - (q >> 5)] : ~0u;
-                }
-#pragma unroll
-                for (u32 k = 0; k < FR; ++k) {
-                    const u32 j = t + w + CL_WAVES * k;
-                    const u32 p = j < tend ? C.todo[j] : 0u;
-                    const u64 b = __ballot(l < nact && ((word[k] >> (p & 31)) & 1u));
-                    if (l == 0 && j < tend) C.res[j] = b != 0 ? 1u : 0u;
-                }
-                __syncthreads();
+                // row, or the bound of (leader, row) may reach alpha (the window's bits in LDS);
+                // the others are rejected by every tile cluster (res 0)
                 if (w == 0) {
+                    const u32 multi = C.multi;
                     u32 n = 0;
                     for (u32 j0 = t; j0 < tend; j0 += 64) {
                         const u32 j = j0 + l;
-                        const bool need = j < tend && C.res[j] != 0;
+                        bool need = false;
+                        if (j < tend) {
+                            const u32 p = C.todo[j];
+                            for (u32 c = 0; c < nact; ++c) need = need || ((multi >> c) & 1u) || wbit(c, p);
+                            C.res[j] = 0;
+                        }
                         const u64 b = __ballot(need);
                         if (need)
                             C.evl[n + __builtin_amdgcn_mbcnt_hi(static_cast<u32>(b >> 32),
@@ -773,6 +789,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 __syncthreads();
                 nev = C.nev;
             }
+            if (a.ctrace && tid == 0) C.tr_nev += nev;
             {
                 // row k of the sub-batch's evaluation list (whichever wave is free takes the next)
                 auto row_at = [&](u32 k) { return a.fbits ? C.evl[k] : t + k; };
@@ -814,8 +831,8 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 // the sequential rule over the sub-batch. Verdicts of clusters whose
                 // representative changed since the evaluation (dirty: accepts, new clusters)
                 // are stale: a position whose walk reaches one is evaluated again by this wave
-                // (accept chains), up to CL_LEADER_EVALS times; after a new cluster, or past
-                // that budget, the rest goes back to all waves
+                // (accept chains), up to CL_LEADER_EVALS times; after a new cluster (unless the
+                // candidate filter runs), or past that budget, the rest goes back to all waves
                 u32 j = t, dirty = 0, budget = CL_LEADER_EVALS;
                 u64 nex = 0, ntot = 0;
                 while (j < tend) {
@@ -824,7 +841,14 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                         // lane-parallel
                         const u32 n = tend - j;
                         const u32 r = l < n ? C.res[j + l] : 0u;
-                        const u64 ev = __ballot(l < n && (r != 0u || C.nact < T));
+                        // (filter: clusters started since the evaluation are the leader rows
+                        // alone here; a set bit makes the row an event)
+                        bool newc = false;
+                        if (a.fbits && l < n) {
+                            const u32 p = C.todo[j + l];
+                            for (u32 c = nact; c < C.nact; ++c) newc = newc || wbit(c, p);
+                        }
+                        const u64 ev = __ballot(l < n && (r != 0u || C.nact < T || newc));
                         const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : min(n, 64u);  // (one wave: 64 at a time)
                         if (l < e) st_agent(&a.state[C.todo[j + l]], klast);
                         ntot += static_cast<u64>(e) * C.nact;
@@ -840,6 +864,10 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                     bool stop = false;  // the rest to all waves
                     for (; c < na; ++c) {
                         if (!fresh && (((dirty >> c) & 1u) || c >= nact)) {
+                            // filter: a cluster started since the evaluation and still its leader
+                            // row alone rejects without an evaluation when the pair's bit is clear
+                            if (a.fbits && !((dirty >> c) & 1u) && !((C.multi >> c) & 1u) && !wbit(c, p))
+                                continue;
                             if (budget == 0) {
                                 stop = true;
                                 break;
@@ -874,7 +902,10 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                     ntot += na;
                     if (na < T) {
                         new_cluster(p, m);
-                        break;  // a new cluster: the rest of the sub-batch to all waves
+                        // a new cluster: without the filter the rest of the sub-batch goes back
+                        // to all waves; with it the walk goes on (its bits are in LDS)
+                        if (!a.fbits) break;
+                        continue;
                     }
                     if (l == 0) st_agent(&a.state[p], klast);
                 }
@@ -910,8 +941,8 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
             tr[11] = C.nexact;
             tr[12] = C.tr_own;
             tr[13] = C.tr_ent;
-            tr[14] = 0;
-            tr[15] = 0;
+            tr[14] = C.tr_nev;
+            tr[15] = static_cast<u64>(__builtin_popcount(C.multi));
         }
     }
 }

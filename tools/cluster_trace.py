@@ -36,7 +36,10 @@ def main():
     gen = synth.SUITESPARSE_REBUILDS.get(args.workload) or getattr(synth, args.workload)
     M, N, rp, ci = gen(args.scale) if args.workload not in synth.SUITESPARSE_REBUILDS else gen()
     t0 = time.perf_counter()
-    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=0.3, tuning={"diag": 2048})
+    tun = {"diag": 2048}
+    if os.environ.get("BSMR_CLUSTER_FILTER") in ("0", "1"):
+        tun["cluster_filter"] = int(os.environ["BSMR_CLUSTER_FILTER"])
+    plan = Plan(M, N, rp, ci, alpha=args.alpha, delta=0.3, tuning=tun)
     wall = time.perf_counter() - t0
     st = plan.stats()
     L = bsmr.lib()
@@ -71,6 +74,11 @@ def main():
            "windows": pct(t[:, 3]), "empty_window_frac": round(float(t[:, 4].sum() / max(1, t[:, 3].sum())), 3),
            "subbatches": pct(t[:, 5]), "evals_per_tile": pct(t[:, 6]),
            "exact_evals_total": int(t[:, 11].sum()),
+           # candidate filter: rows a tile evaluated (the rest were skipped by their bits), and
+           # clusters holding more than their leader row (never skipped)
+           "evaluated_rows_total": int(t[:, 14].sum()), "multi_clusters_total": int(t[:, 15].sum()),
+           "tiles_with_multi": int((t[:, 15] > 0).sum()),
+           "filter_ms": round(float(st.get("cluster_filter_ms", 0.0)), 2),
            # where a tile's life goes (sums over tiles, fraction of summed lifetimes)
            "life_split": {k: round(float(t[:, i].sum() / max(1, (e - b).sum())), 3)
                           for k, i in (("scan_and_spin", 8), ("evaluate", 9), ("leader", 10))},
