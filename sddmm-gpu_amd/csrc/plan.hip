@@ -756,9 +756,10 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 ++C.tr_sub;
                 if (a.ctrace) C.tr_t0 = now_ticks();
             }
-            // with the candidate filter a sub-batch is the whole window (skipped rows cost a bit
-            // test, not an evaluation)
-            const u32 tend = min(ntodo, t + (a.fbits ? CL_WIN : CL_SUB));
+            // with the candidate filter a sub-batch is the whole window while every tile cluster
+            // is its leader row alone (skipped rows cost a bit test, not an evaluation); once one
+            // holds more rows, accepts are common and short sub-batches re-evaluate less
+            const u32 tend = min(ntodo, t + (a.fbits && C.multi == 0 ? CL_WIN : CL_SUB));
             u32 nev = tend - t;
             if (a.fbits) {
                 // a row needs its evaluation only if some tile cluster holds more than its leader
@@ -2360,30 +2361,38 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     BSMR_HIP(hipGetLastError());
     // candidate filter: an MFMA pass over every pair of rows bounds their similarity, so the
     // chain skips the pairs that cannot reach alpha (cluster_filter.hip)
+    // cluster_filter = 1: from the start; auto (-1, from filter_min_rows rows): after a first
+    // launch of about 1,536 clusters without it, when those took at least one position in four
+    // (most positions then start their own cluster and the chain compares nearly every pair;
+    // patterns whose rows join a few clusters finish cheaply without it: cop20k-like alpha 0.1
+    // 87 ms unfiltered against a 125 ms filter pass, profiles/r04ze)
     DevBuf<u32> fbits;
     u32 fW = 0;
     filter_used = false;
     filter_ms = 0.f;
-    if (cluster_filter != 0 && !exact_all && alpha >= 0.01f && M - z >= 2 &&
-        (cluster_filter == 1 || M >= filter_min_rows)) {
+    const bool filter_ok = cluster_filter != 0 && !exact_all && alpha >= 0.01f && M - z >= 2 &&
+                           (cluster_filter == 1 || M >= filter_min_rows);
+    auto build_filter = [&]() -> int {
         size_t fr = 0, tot = 0;
         BSMR_HIP(hipMemGetInfo(&fr, &tot));
         const u64 Kp = (nbpr + 63ull) / 64 * 64;
         const u64 need = static_cast<u64>(M) * Kp * 2 + sim_filter_words(M) * 4 + static_cast<u64>(M) * 8;
-        if (need <= fr / 4) {
-            hipEvent_t f0, f1;
-            BSMR_HIP(hipEventCreate(&f0));
-            BSMR_HIP(hipEventCreate(&f1));
-            BSMR_HIP(hipEventRecord(f0, s));
-            BSMR_CHECK(build_sim_filter(pmeta.data(), enc.data(), M, nbpr, B, keptMask, alpha, fbits, fW, s));
-            BSMR_HIP(hipEventRecord(f1, s));
-            BSMR_HIP(hipEventSynchronize(f1));
-            BSMR_HIP(hipEventElapsedTime(&filter_ms, f0, f1));
-            BSMR_HIP(hipEventDestroy(f0));
-            BSMR_HIP(hipEventDestroy(f1));
-            filter_used = true;
-        }
-    }
+        if (need > fr / 4) return BSMR_OK;  // (the chain runs unfiltered)
+        hipEvent_t f0, f1;
+        BSMR_HIP(hipEventCreate(&f0));
+        BSMR_HIP(hipEventCreate(&f1));
+        BSMR_HIP(hipEventRecord(f0, s));
+        BSMR_CHECK(build_sim_filter(pmeta.data(), enc.data(), M, nbpr, B, keptMask, alpha, fbits, fW, s));
+        BSMR_HIP(hipEventRecord(f1, s));
+        BSMR_HIP(hipEventSynchronize(f1));
+        BSMR_HIP(hipEventElapsedTime(&filter_ms, f0, f1));
+        BSMR_HIP(hipEventDestroy(f0));
+        BSMR_HIP(hipEventDestroy(f1));
+        filter_used = true;
+        return BSMR_OK;
+    };
+    if (filter_ok && cluster_filter == 1) BSMR_CHECK(build_filter());
+    bool probe = filter_ok && cluster_filter != 1;
     ClusterArgs ca{};
     ca.fbits = filter_used ? fbits.data() : nullptr;
     ca.fW = fW;
@@ -2427,7 +2436,7 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     u32 c0 = 1;
     u32 last_valid = 0;
     while (c0 <= M) {  // at most M - z clusters
-        const u32 tiles = std::min<u32>(tilesMax, (M + 1 - c0 + T - 1) / T);
+        const u32 tiles = std::min<u32>(probe ? std::max<u32>(1, 1536 / T) : tilesMax, (M + 1 - c0 + T - 1) / T);
         const u32 R = tiles * T;
         ca.c0 = c0;
         BSMR_HIP(hipMemsetAsync(ctrl.data() + 6, 0, sizeof(u32), s));  // ticket counter
@@ -2458,6 +2467,16 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
         exact_evals = (static_cast<u64>(hctrl[3]) << 32) | hctrl[2];
         total_evals = (static_cast<u64>(hctrl[5]) << 32) | hctrl[4];
         if (done) break;
+        if (probe) {
+            // the probe launch's last cluster started at position hst[R - 1] - 2
+            probe = false;
+            const u32 pos = hst[R - 1] - 2;
+            if (pos >= z && 4ull * R >= static_cast<u64>(pos - z + 1)) {
+                BSMR_CHECK(build_filter());
+                ca.fbits = filter_used ? fbits.data() : nullptr;
+                ca.fW = fW;
+            }
+        }
         c0 += R;
     }
     (void)last_valid;
