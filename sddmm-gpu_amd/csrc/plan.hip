@@ -17,7 +17,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <queue>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1527,6 +1529,24 @@ std::shared_ptr<const Plan::RowBlockLayout> Plan::rowblock_layout(u32 rowBytes, 
 }
 
 // Row-block launch layout over panels [pa, pb) (the whole plan, or one row-panel shard).
+// the layout's host passes over [0, n) on up to 16 threads: f(thread, begin, end), contiguous
+// ranges, each index visited once (results written per index are independent of the split)
+template <class F>
+static void par_for(size_t n, F&& f, size_t serial_below = 2048) {
+    const unsigned T = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < serial_below || T == 1) {
+        f(0u, size_t{0}, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t chunk = (n + T - 1) / T;
+    for (unsigned t = 0; t < T; ++t) {
+        const size_t a = t * chunk, b = std::min(n, a + chunk);
+        if (a < b) th.emplace_back([&f, t, a, b]() { f(t, a, b); });
+    }
+    for (auto& x : th) x.join();
+}
+
 int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
                                 bool orig) const {
     L.rowBytes = 0;
@@ -1540,6 +1560,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         set_error("original-order row blocks cover the whole plan only");
         return BSMR_ERR_INVALID;
     }
+    // BSMR_DIAG & 524288: section times of this build to stderr (host-side layout cost)
+    auto lap_t = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!(diag & 524288)) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[rb layout %u B] %-12s %8.1f ms\n", rowBytes, what,
+                     std::chrono::duration<double, std::milli>(t - lap_t).count());
+        lap_t = t;
+    };
     const u32 qa = orig ? 0 : 16 * pa, qend = orig ? M : std::min(R, 16 * pb);
     const u32 Rs = qend > qa ? qend - qa : 0;  // (reordered) rows of the range
     int cus = 256;
@@ -1689,6 +1718,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_HIP(hipStreamSynchronize(s));
         for (u32 b = 1; b < nRB; ++b) rbEnd[b] = std::max(rbEnd[b], rbEnd[b - 1]);
     }
+    lap("sort+meta");
     // column ranges: NCR = 8 m ranges of (nearly) equal residual count; XCD x owns ranges
     // [x m, (x + 1) m). m makes one range's B columns (N rowBytes / NCR) fit an L2 budget: the
     // items of an XCD are ordered by range, so the B columns an item gathers were brought into
@@ -1710,18 +1740,27 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         // column weight: its entries, plus (item_sched) piece_weight per column-run piece it
         // heads, so the XCDs' ranges carry equal modeled cost rather than equal entry counts
         // (mycielskian: the last XCD's range carried 10 % more piece work and ended 10 % later)
-        std::vector<double> cnt(N + 1, 0.0);
-        for (u32 b = 0, lo = 0; b < nRB; ++b) {
-            const u32 hi = rbEnd[b];
-            u32 run = 0;
-            for (u32 i = lo; i < hi; ++i) {
-                const u32 c = hmeta[i] & CM;
-                const bool start = i == lo || c != (hmeta[i - 1] & CM) || run >= piece_max;
-                run = start ? 1 : run + 1;
-                cnt[c] += 1.0 + (item_cost_cuts && start ? piece_weight : 0.0);
+        // (per-thread sums over row blocks, added in thread order: with the default integral
+        // weights every partial sum is exact, so the cuts do not depend on the split)
+        std::vector<std::vector<double>> cntT(16);
+        par_for(nRB, [&](unsigned t, size_t b0, size_t b1) {
+            std::vector<double>& cnt = cntT[t];
+            cnt.assign(N + 1, 0.0);
+            for (size_t b = b0; b < b1; ++b) {
+                const u32 lo = b ? std::max(rbEnd[b - 1], 0u) : 0u, hi = rbEnd[b];
+                u32 run = 0;
+                for (u32 i = lo; i < hi; ++i) {
+                    const u32 c = hmeta[i] & CM;
+                    const bool start = i == lo || c != (hmeta[i - 1] & CM) || run >= piece_max;
+                    run = start ? 1 : run + 1;
+                    cnt[c] += 1.0 + (item_cost_cuts && start ? piece_weight : 0.0);
+                }
             }
-            lo = std::max(lo, hi);
-        }
+        }, 16);
+        std::vector<double> cnt(N + 1, 0.0);
+        for (const auto& ct : cntT)
+            if (!ct.empty())
+                for (u32 c = 0; c <= N; ++c) cnt[c] += ct[c];
         double tot = 0;
         for (u32 c = 0; c < N; ++c) tot += cnt[c];
         double run = 0;
@@ -1732,13 +1771,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         }
         for (; x < NCR; ++x) cuts[x] = N;
     }
+    lap("cuts");
     // segments (rb, range k): entries of rb in range k + 1/NCR of rb's tiles; cost = entries +
     // column-run pieces (one B column each) + 16 per tile
     const size_t nseg = static_cast<size_t>(nRB) * NCR;
     std::vector<u32> se0(nseg), se1(nseg), st0(nseg), st1(nseg), spc(nseg, 0);
     std::vector<double> cost(nseg);
     std::vector<u64> piecesRB(nRB, 0);
-    for (u32 b = 0; b < nRB; ++b) {
+    par_for(nRB, [&](unsigned, size_t bb0, size_t bb1) {
+    for (u32 b = static_cast<u32>(bb0); b < bb1; ++b) {
         const u32 eb0 = b ? rbEnd[b - 1] : 0, eb1 = rbEnd[b];
         const u32 p0 = std::min(pa + b * (RBr / 16), pb), p1 = std::min(pa + (b + 1) * (RBr / 16), pb);
         // kept tiles of the row block: positions [t0, t0 + nt) of the kept list
@@ -1769,6 +1810,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             cost[i] = (se1[i] - se0[i]) + piece_weight * spc[i] + 16.0 * (st1[i] - st0[i]);
         }
     }
+    }, 16);
+    lap("segments");
     // chunks. A row block is split by the column ranges (its items then read B from their own
     // XCD's L2) when it is big enough for >= 8 items of a one-round launch, or (m > 1) when its
     // column runs would gather more B rows than NCR restagings of its A rows cost; a smaller one
@@ -2019,6 +2062,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             if (cb[b] > 2 * target)
                 std::fprintf(stderr, "[rb layout]   block %u cost %.0f split %d nu %u\n", b, cb[b], split[b], nu[b]);
     }
+    lap("chunks");
     std::vector<uint4> items;
     std::vector<u32> ends;
     // range sweep: per XCD, W = perBucket persistent workgroups (one per CU). Every row block
@@ -2132,6 +2176,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             ends[j * XCD_BUCKETS + x] = lends[x][j];
         }
     }
+    lap("items");
     // column-run pieces: each item's entries [e0, e1) cut at column changes and every
     // piece_max (<= RB_PIECE_MAX) entries; piece {first entry, column | (length - 1) << 22}. A workgroup's NG
     // row-groups take one piece each per phase, so phase ph runs the item's pieces
@@ -2144,37 +2189,53 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     for (size_t i = 0; i < items.size(); ++i)
         ient[i] = make_uint2(items[i].w, (items[i].y == items[i].z && items[i].w == ends[i]) ? 0u
                                                                                           : ends[i] - items[i].w);
-    std::vector<uint2> pieces;
-    pieces.reserve(n / 4 + items.size());
-    std::vector<uint2> mine;
-    for (size_t i = 0; i < items.size(); ++i) {
-        const u32 ea = items[i].w, eb = ends[i];
-        mine.clear();
-        for (u32 e = ea; e < eb;) {
-            const u32 col = hmeta[e] & CM;
-            u32 f = e + 1;
-            while (f < eb && f - e < piece_max && (hmeta[f] & CM) == col) ++f;
-            mine.push_back(make_uint2(e, col | ((f - e - 1) << 22)));
-            e = f;
+    // (per item on the host threads, then placed in item order)
+    std::vector<std::vector<uint2>> ipc(items.size());
+    par_for(items.size(), [&](unsigned, size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            std::vector<uint2>& mine = ipc[i];
+            const u32 ea = items[i].w, eb = ends[i];
+            for (u32 e = ea; e < eb;) {
+                const u32 col = hmeta[e] & CM;
+                u32 f = e + 1;
+                while (f < eb && f - e < piece_max && (hmeta[f] & CM) == col) ++f;
+                mine.push_back(make_uint2(e, col | ((f - e - 1) << 22)));
+                e = f;
+            }
+            for (size_t w0 = 0; w0 < mine.size(); w0 += NG)
+                std::stable_sort(mine.begin() + w0, mine.begin() + std::min<size_t>(mine.size(), w0 + NG),
+                                 [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
         }
-        for (size_t w0 = 0; w0 < mine.size(); w0 += NG)
-            std::stable_sort(mine.begin() + w0, mine.begin() + std::min<size_t>(mine.size(), w0 + NG),
-                             [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
-        items[i].w = static_cast<u32>(pieces.size());
-        pieces.insert(pieces.end(), mine.begin(), mine.end());
-        ends[i] = static_cast<u32>(pieces.size());
-    }
+    });
+    std::vector<size_t> poff(items.size() + 1, 0);
+    for (size_t i = 0; i < items.size(); ++i) poff[i + 1] = poff[i] + ipc[i].size();
+    std::vector<uint2> pieces(poff.back());
+    L.itemStat.assign(items.size(), make_uint4(0, 0, 0, 0));
+    std::vector<u64> ientc(items.size(), 0);
+    std::vector<char> ipad(items.size(), 0);
+    par_for(items.size(), [&](unsigned, size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            const bool pad = items[i].y == items[i].z && items[i].w == ends[i];
+            std::copy(ipc[i].begin(), ipc[i].end(), pieces.begin() + poff[i]);
+            std::vector<uint2>().swap(ipc[i]);
+            items[i].w = static_cast<u32>(poff[i]);
+            ends[i] = static_cast<u32>(poff[i + 1]);
+            ipad[i] = pad;
+            if (pad) continue;
+            u64 ent = 0;
+            for (u32 k = items[i].w; k < ends[i]; ++k) ent += (pieces[k].y >> 22) + 1;
+            ientc[i] = ent;
+            L.itemStat[i] = make_uint4(items[i].x, items[i].z - items[i].y, static_cast<u32>(ent),
+                                       ends[i] - items[i].w);
+        }
+    });
     L.rbCost.assign(nRB, 0.0);
     L.nWorkItems = 0;
-    L.itemStat.assign(items.size(), make_uint4(0, 0, 0, 0));
     for (size_t i = 0; i < items.size(); ++i) {
         const uint4 it = items[i];
-        if (it.y == it.z && it.w == ends[i]) continue;  // padding
+        if (ipad[i]) continue;  // padding
         ++L.nWorkItems;
-        u64 ent = 0;
-        for (u32 k = it.w; k < ends[i]; ++k) ent += (pieces[k].y >> 22) + 1;
-        L.itemStat[i] = make_uint4(it.x, it.z - it.y, static_cast<u32>(ent), ends[i] - it.w);
-        L.rbCost[it.x] += static_cast<double>(ent) + shard_piece_weight * (ends[i] - it.w) +
+        L.rbCost[it.x] += static_cast<double>(ientc[i]) + shard_piece_weight * (ends[i] - it.w) +
                           16.0 * (it.z - it.y) + RBr;
     }
     L.nItems = static_cast<u32>(items.size());
@@ -2187,6 +2248,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     L.itemEnt.release();
     L.runs.release();
     L.itemRuns.release();
+    lap("pieces");
     if (staged && n) {
         // slots: per item, its entries sorted by CSR position (segmented radix sort on the device)
         BSMR_CHECK(L.itemEnt.upload(ient.data(), ient.size(), s));
@@ -2199,8 +2261,10 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_CHECK(dsb.upload(segb.data(), segb.size(), s));
         BSMR_CHECK(dse.upload(sege.data(), sege.size(), s));
         std::vector<u32> hl(n);
-        for (size_t i = 0; i < ient.size(); ++i)
-            for (u32 t = 0; t < ient[i].y; ++t) hl[ient[i].x + t] = t;
+        par_for(ient.size(), [&](unsigned, size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; ++i)
+                for (u32 t = 0; t < ient[i].y; ++t) hl[ient[i].x + t] = t;
+        });
         BSMR_CHECK(lidx.upload(hl.data(), n, s));
         BSMR_CHECK(skeys.alloc(n));
         BSMR_CHECK(svals.alloc(n));
@@ -2236,25 +2300,37 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             BSMR_HIP(hipMemcpyAsync(hpos.data(), L.sortedPos.data(), n * sizeof(u32),
                                     hipMemcpyDeviceToHost, s));
             BSMR_HIP(hipStreamSynchronize(s));
-            std::vector<uint2> hr;
-            hr.reserve(n / 16 + ient.size());
-            std::vector<uint2> hir(ient.size(), make_uint2(0, 0));
-            bool fits = true;
-            for (size_t i = 0; i < ient.size() && fits; ++i) {
-                const u32 e0 = ient[i].x, len = ient[i].y;
-                const size_t r0 = hr.size();
-                for (u32 t = 0; t < len;) {
-                    // a run is one wave store: at most 64 consecutive positions (an unsplit
-                    // original-order item is one long run, which would leave all but one wave
-                    // idle in the store pass)
-                    u32 u = t + 1;
-                    while (u < len && u - t < 64 && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
-                    hr.push_back(make_uint2(hpos[e0 + t], t | ((u - t) << 16)));
-                    t = u;
+            // (per item on the host threads, then placed in item order)
+            std::vector<std::vector<uint2>> ir(ient.size());
+            std::vector<char> over(ient.size(), 0);
+            par_for(ient.size(), [&](unsigned, size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i) {
+                    const u32 e0 = ient[i].x, len = ient[i].y;
+                    for (u32 t = 0; t < len;) {
+                        // a run is one wave store: at most 64 consecutive positions (an unsplit
+                        // original-order item is one long run, which would leave all but one
+                        // wave idle in the store pass)
+                        u32 u = t + 1;
+                        while (u < len && u - t < 64 && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
+                        ir[i].push_back(make_uint2(hpos[e0 + t], t | ((u - t) << 16)));
+                        t = u;
+                    }
+                    over[i] = ir[i].size() > NT;
                 }
-                hir[i] = make_uint2(static_cast<u32>(r0), static_cast<u32>(hr.size() - r0));
-                fits = hir[i].y <= NT;
+            });
+            bool fits = true;
+            std::vector<uint2> hir(ient.size(), make_uint2(0, 0));
+            size_t nr = 0;
+            for (size_t i = 0; i < ient.size(); ++i) {
+                fits = fits && !over[i];
+                hir[i] = make_uint2(static_cast<u32>(nr), static_cast<u32>(ir[i].size()));
+                nr += ir[i].size();
             }
+            std::vector<uint2> hr(fits ? nr : 0);
+            if (fits)
+                par_for(ient.size(), [&](unsigned, size_t i0, size_t i1) {
+                    for (size_t i = i0; i < i1; ++i) std::copy(ir[i].begin(), ir[i].end(), hr.begin() + hir[i].x);
+                });
             if (fits) {
                 BSMR_CHECK(L.runs.upload(hr.data(), std::max<size_t>(hr.size(), 1), s));
                 BSMR_CHECK(L.itemRuns.upload(hir.data(), std::max<size_t>(hir.size(), 1), s));
@@ -2271,6 +2347,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         L.out.release();
         L.outPacked = true;
     }
+    lap("staged");
     // the sweep kernel stores by runs only; without a run table the items (independent, in any
     // order) run on k_sddmm_rb, one workgroup each
     L.sweep = sweep && L.outRuns;
@@ -2301,6 +2378,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_CHECK(L.rowIds.upload(ids.data(), std::max<u32>(M, 1), s));
         BSMR_HIP(hipStreamSynchronize(s));
     }
+    lap("upload");
     L.tileMin = tileMin;
     L.nTilesKept = static_cast<u32>(hkept.size());
     L.nDemoted = nd;
