@@ -213,6 +213,8 @@ constexpr u32 CL_LDS_BUDGET = 148 * 1024;  // representatives (the control block
 // accept chains the leader resolves alone (re-evaluating one position at a time) before it
 // hands the rest of a sub-batch back to all waves
 constexpr u32 CL_LEADER_EVALS = 16;
+// encoding loads per lane the leader keeps in flight when it fills or updates a representative
+constexpr u32 CL_ENC_B = 8;
 // encoding chunks (256 entries) of a row whose loads are issued together (registers: 4 per chunk)
 #ifndef BSMR_CL_PRE_CH
 #define BSMR_CL_PRE_CH 2
@@ -548,13 +550,28 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
     };
     auto wbit = [&](u32 c, u32 p) -> bool { return (C.wbits[c][(p >> 5) - C.wb0] >> (p & 31)) & 1u; };
     // leader: start a new tile cluster (index C.nact) at position p (metadata m)
+    // leader: the row's encoding entries (metadata m), CL_ENC_B loads per lane in flight per
+    // round trip, each handed to body in turn (a load -> LDS store loop paid one round trip per 64
+    // entries, and new clusters are the chain's critical path once the candidate filter skips
+    // the evaluations)
+    auto for_enc = [&](uint4 m, auto&& body) {
+        for (u32 e0 = 0; e0 < m.y; e0 += 64 * CL_ENC_B) {
+            u32 v[CL_ENC_B];
+#pragma unroll
+            for (u32 k = 0; k < CL_ENC_B; ++k) {  // clamped, unconditional (m.y >= 1 here)
+                const u32 e = e0 + l + 64 * k;
+                const u32 x = a.enc[m.x + min(e, m.y - 1)];
+                v[k] = x;
+            }
+#pragma unroll
+            for (u32 k = 0; k < CL_ENC_B; ++k)
+                if (e0 + l + 64 * k < m.y) body(v[k]);
+        }
+    };
     auto new_cluster = [&](u32 p, uint4 m) {
         const u32 c = C.nact;
         if (a.fbits) load_wbits(c, p);
-        for (u32 e = l; e < m.y; e += 64) {
-            const u32 ent = a.enc[m.x + e];
-            reps[(ent & 0xFFFFu) * TS + c] = ent >> 16;
-        }
+        for_enc(m, [&](u32 ent) { reps[(ent & 0xFFFFu) * TS + c] = ent >> 16; });
         if (l == 0) {
             set_norm(c, m.z);
             C.S1R[c] = m.w;
@@ -567,8 +584,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
     // leader: position p (metadata m) joins tile cluster c
     auto accept = [&](u32 p, uint4 m, u32 c) {
         u32 dsr = 0, ds1 = 0;
-        for (u32 e = l; e < m.y; e += 64) {
-            const u32 ent = a.enc[m.x + e];
+        for_enc(m, [&](u32 ent) {  // (a row's blocks are distinct: no two lanes update one slot)
             const u32 blk = ent & 0xFFFFu, cnt = ent >> 16;
             const u32 o = reps[blk * TS + c], nv = o + cnt;
             reps[blk * TS + c] = nv;
@@ -576,7 +592,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 dsr += nv * nv - o * o;
                 ds1 += cnt;
             }
-        }
+        });
         dsr = wave_sum(dsr);
         ds1 = wave_sum(ds1);
         if (l == 0) {
@@ -768,14 +784,19 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                 // row, or the bound of (leader, row) may reach alpha (the window's bits in LDS);
                 // the others are rejected by every tile cluster (res 0)
                 if (w == 0) {
-                    const u32 multi = C.multi;
+                    // (every row needs its evaluation while a tile cluster holds several rows;
+                    // the bit tests without short-circuit branches, so their LDS reads overlap)
+                    const bool anyMulti = (C.multi & ((1u << nact) - 1u)) != 0;
+                    const u32 wb0 = C.wb0;
                     u32 n = 0;
                     for (u32 j0 = t; j0 < tend; j0 += 64) {
                         const u32 j = j0 + l;
                         bool need = false;
                         if (j < tend) {
-                            const u32 p = C.todo[j];
-                            for (u32 c = 0; c < nact; ++c) need = need || ((multi >> c) & 1u) || wbit(c, p);
+                            const u32 p = C.todo[j], k = (p >> 5) - wb0;
+                            u32 bits = 0;
+                            for (u32 c = 0; c < nact; ++c) bits |= C.wbits[c][k];
+                            need = anyMulti || ((bits >> (p & 31)) & 1u);
                             C.res[j] = 0;
                         }
                         const u64 b = __ballot(need);
@@ -848,8 +869,10 @@ __global__ __launch_bounds__(64 * CL_WAVES) void k_cluster(ClusterArgs a) {
                         // alone here; a set bit makes the row an event)
                         bool newc = false;
                         if (a.fbits && l < n) {
-                            const u32 p = C.todo[j + l];
-                            for (u32 c = nact; c < C.nact; ++c) newc = newc || wbit(c, p);
+                            const u32 p = C.todo[j + l], k = (p >> 5) - C.wb0, na = C.nact;
+                            u32 bits = 0;
+                            for (u32 c = nact; c < na; ++c) bits |= C.wbits[c][k];
+                            newc = (bits >> (p & 31)) & 1u;
                         }
                         const u64 ev = __ballot(l < n && (r != 0u || C.nact < T || newc));
                         const u32 e = ev ? static_cast<u32>(__builtin_ctzll(ev)) : min(n, 64u);  // (one wave: 64 at a time)
