@@ -132,6 +132,23 @@ def test_cluster_filter_same_permutation(name, alpha):
     assert s_on["exact_similarity_evals"] == s_off["exact_similarity_evals"]
 
 
+@pytest.mark.parametrize("M,N,per_row,alpha", [(300, 400000, 100, 0.3), (600, 250000, 80, 0.1),
+                                               (400, 180000, 150, 0.5)])
+def test_cluster_filter_wide_tiles(M, N, per_row, alpha):
+    """Wide patterns at the block-count ceiling of calculateBlockSize (~6,100 column blocks, so
+    a clustering tile holds T = 6 representatives, as for reddit; the small cases above run
+    T = 8): the filtered permutation equals the oracle's."""
+    M, N, rp, ci = synth.random_rows(M, N, per_row, seed=M + N, zipf=1.05)
+    gp = Plan(M, N, rp, ci, alpha=alpha, delta=0.3, free_mem_bytes=FREE,
+              tuning=tuning_from_env({"BSMR_CLUSTER_FILTER": "1"}))
+    st = gp.stats()
+    assert st["cluster_filter_used"] == 1
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    rows, ncl, _ = O.row_reorder(c, np.float32(alpha), O.block_size(M, N, FREE))
+    assert st["num_clusters"] == ncl
+    assert np.array_equal(gp.array("reorderedRows"), rows)
+
+
 @pytest.mark.parametrize("scale,alpha", [(0.02, 0.3), (0.05, 0.3), (0.05, 0.1), (0.05, 0.7)])
 def test_cluster_filter_reddit_like(scale, alpha):
     """A power-law graph (almost every position starts its own cluster, so the chain compares
