@@ -2537,7 +2537,9 @@ int Plan::build_rows(const u32* h_rowptr, const u32* h_col) {
     u32 c0 = 1;
     u32 last_valid = 0;
     while (c0 <= M) {  // at most M - z clusters
-        const u32 tiles = std::min<u32>(probe ? std::max<u32>(1, 1536 / T) : tilesMax, (M + 1 - c0 + T - 1) / T);
+        // (the probe launch too stays within tilesMax: the exact path's scratch has tilesMax rows)
+        const u32 tiles = std::min<u32>(probe ? std::min<u32>(tilesMax, std::max<u32>(1, 1536 / T)) : tilesMax,
+                                        (M + 1 - c0 + T - 1) / T);
         const u32 R = tiles * T;
         ca.c0 = c0;
         BSMR_HIP(hipMemsetAsync(ctrl.data() + 6, 0, sizeof(u32), s));  // ticket counter
