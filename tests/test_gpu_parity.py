@@ -166,6 +166,20 @@ def test_cluster_filter_reddit_like(scale, alpha):
     assert stats[0]["total_similarity_evals"] == stats[1]["total_similarity_evals"]
 
 
+@pytest.mark.parametrize("batch", [0, 600])
+def test_cluster_filter_auto_probe(batch):
+    """The default policy (probe launch without the filter, then the filter) on a pattern above
+    its row threshold, with the default and a small clusters-per-launch setting (the probe then
+    shrinks to the launch's scratch): the permutation equals the unfiltered chain's."""
+    M, N, rp, ci = synth.reddit_like(0.2)
+    auto = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, cluster_batch=batch)
+    off = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, cluster_batch=batch,
+               tuning=tuning_from_env({"BSMR_CLUSTER_FILTER": "0"}))
+    assert M >= 32768 and auto.stats()["cluster_filter_used"] == 1
+    assert auto.stats()["num_clusters"] == off.stats()["num_clusters"]
+    assert np.array_equal(auto.array("reorderedRows"), off.array("reorderedRows"))
+
+
 def test_cluster_filter_nips_like_bit_exact():
     """nips-like (C1/C2's pattern) with the filter forced on: plan arrays equal the oracle's."""
     M, N, rp, ci = nips_like_case()
