@@ -1618,12 +1618,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // staged 512-byte rows (C4 reddit-like x1 fp32 K = 128): 8 MiB ranges too, half the A
     // restaging for a B range twice the L2 (4.01 -> 3.89 ms over three alternating runs,
     // profiles/r03y; C3 fp16 K = 256 neutral)
-    // ... but at least two ranges per XCD: one range of the XCD's whole B share ran C4 x0.5 (7.5
-    // MiB per XCD) at 1.33 ms against 1.00 ms with two (profiles/r04x); x1 keeps two 7.5 MiB ranges
+    // ... but at least two ranges per XCD when its B share exceeds its 4 MiB L2: one range of the
+    // whole share ran C4 x0.5 (7.5 MiB per XCD) at 1.33 ms against 1.00 ms with two
+    // (profiles/r04x); x1 keeps two 7.5 MiB ranges; a share that fits the L2 stays one range
+    // (mycielskian16 K = 128, 3 MiB per XCD: 166 us against 181 us with two; profiles/r04zr)
     const bool staged512 = stagedWanted && item_cost_cuts && rowBytes == 512;
     const double shareKb = static_cast<double>(N) * rowBytes / XCD_BUCKETS / 1024.0;
     const u32 l2Kb = l2_range_user ? l2_range_kb
-                     : staged512 ? std::min<u32>(8192u, std::max<u32>(64u, static_cast<u32>(std::ceil(shareKb / 2)) + 1))
+                     : staged512 ? (shareKb > 4096.0 ? std::min<u32>(8192u, static_cast<u32>(std::ceil(shareKb / 2)) + 1)
+                                                     : 8192u)
                      : bigRows ? 8192u
                      : stagedWanted ? l2_range_kb_staged : l2_range_kb;
     u32 RBr = rowblock_rows(rowBytes, ldsKb, Rs);

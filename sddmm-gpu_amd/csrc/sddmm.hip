@@ -1380,7 +1380,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_sweep(RbArgs a) {
 
 template <int DT, int RBY>
 void (*pick_rb(const u32 NT, const bool pairs, const bool sweep))(RbArgs) {
-    if constexpr (RBY >= 256) {  // (no pairs at 128-byte rows: launch_rb enables them from 256)
+    if constexpr (RBY >= 256) {  // (launch_rb enables pairs from 512-byte rows)
         if (sweep && NT == 1024) return k_sddmm_rb_sweep<DT, RBY, 1024>;
         if (pairs) return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024> : k_sddmm_rb_pair<DT, RBY, 512>;
     }
@@ -1521,10 +1521,12 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.itemEnt = L.itemEnt.data();
     a.runs = L.outRuns ? L.runs.data() : nullptr;
     a.itemRuns = L.outRuns ? L.itemRuns.data() : nullptr;
-    // pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 256 bytes, an even number
+    // pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 512 bytes, an even number
     // of list positions per XCD; not under the profiling ablations (trace, staging only, B in
-    // L2, no stores)
-    a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 256 && L.nTilesKept == 0 &&
+    // L2, no stores). 256-byte rows run their items unpaired: mycielskian15 / 16 K = 64 56.9 /
+    // 114.6 us paired against 50.1 / 108.9 unpaired; 512-byte rows gain (C4 x0.5 1.029 -> 0.984
+    // ms), 1-2 KiB rows and C3 are neutral (profiles/r04zt)
+    a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nTilesKept == 0 &&
                       L.nItems % (2 * XCD_BUCKETS) == 0 && !a.stageNt && a.lateB &&
                       !(p.diag & (8u | 32u | 64u | 128u | 16384u))
                   ? 1u

@@ -12,6 +12,14 @@ case "$CFG" in
     C4) ARGS="--workload reddit_like --scale 0.5 --K 128 --dtype f32" ;;
     C4x1) ARGS="--workload reddit_like --scale 1.0 --K 128 --dtype f32" ;;
     C5u) ARGS="--workload dlmc_like --mask uniform --K 512 --dtype bf16" ;;
+    M15k64) ARGS="--workload mycielskian15 --K 64 --alpha 0.3 --delta 0.1" ;;
+    M16k128) ARGS="--workload mycielskian16 --K 128 --alpha 0.3 --delta 0.1" ;;
+    M14k128) ARGS="--workload mycielskian14 --K 128 --alpha 0.5 --delta 0.3" ;;
+    M15k256) ARGS="--workload mycielskian15 --K 256 --alpha 0.5 --delta 0.7" ;;
+    M16k256) ARGS="--workload mycielskian16 --K 256 --alpha 0.5 --delta 0.7" ;;
+    M16k512) ARGS="--workload mycielskian16 --K 512 --alpha 0.5 --delta 0.5" ;;
+    M16k64) ARGS="--workload mycielskian16 --K 64 --alpha 0.3 --delta 0.1" ;;
+    T128) ARGS="--workload Trefethen_20000 --K 128 --alpha 0.7 --delta 0.5" ;;
     *) echo "unknown config $CFG" >&2; exit 2 ;;
 esac
 n=0
