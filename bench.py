@@ -388,8 +388,9 @@ def kernel_name(st, st_after, K, dtype, layout):
         rows = st_after["rb_rows"][i]
         nt = 1024 if rby * rows > 80 * 1024 else 512
         # sddmm.hip launch_rb: staged output (P > 8 MiB) by runs, no kept MFMA tile, rows of
-        # >= 256 bytes -> the pair kernel (two list positions per workgroup)
-        pair = 4 * st["nnz"] > (8 << 20) and rby >= 256 and not st_after["rb_tiles"][i]
+        # >= 512 bytes, >= 4096 items -> the pair kernel (two list positions per workgroup)
+        pair = (4 * st["nnz"] > (8 << 20) and rby >= 512 and st_after["rb_items"][i] >= 4096
+                and not st_after["rb_tiles"][i])
         name = "k_sddmm_rb_pair" if pair else "k_sddmm_rb"
         return (f"{name}<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
                 f"rows per block: residual entries; {tiles}"

@@ -1521,12 +1521,14 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.itemEnt = L.itemEnt.data();
     a.runs = L.outRuns ? L.runs.data() : nullptr;
     a.itemRuns = L.outRuns ? L.itemRuns.data() : nullptr;
-    // pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 512 bytes, an even number
-    // of list positions per XCD; not under the profiling ablations (trace, staging only, B in
-    // L2, no stores). 256-byte rows run their items unpaired: mycielskian15 / 16 K = 64 56.9 /
-    // 114.6 us paired against 50.1 / 108.9 unpaired; 512-byte rows gain (C4 x0.5 1.029 -> 0.984
-    // ms), 1-2 KiB rows and C3 are neutral (profiles/r04zt)
-    a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nTilesKept == 0 &&
+    // pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 512 bytes, at least 4096
+    // items (16 rounds of the chip's workgroup slots), an even number of list positions per XCD;
+    // not under the profiling ablations (trace, staging only, B in L2, no stores). A pair is two
+    // items long, so short lists lose to the tail: mycielskian15 K = 64 / 128 (832 / 728 items)
+    // 56.9 / 74.6 us paired against 50.1 / 66.5 unpaired, mycielskian16 K = 64 114.6 against
+    // 108.9; C4 (8-30 K items) gains (x0.5 1.029 -> 0.984 ms), C3, mycielskian16 K = 128 and
+    // 1-2 KiB rows are neutral (profiles/r04zt, r04zw)
+    a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= 4096 && L.nTilesKept == 0 &&
                       L.nItems % (2 * XCD_BUCKETS) == 0 && !a.stageNt && a.lateB &&
                       !(p.diag & (8u | 32u | 64u | 128u | 16384u))
                   ? 1u

@@ -19,6 +19,7 @@ case "$CFG" in
     M16k256) ARGS="--workload mycielskian16 --K 256 --alpha 0.5 --delta 0.7" ;;
     M16k512) ARGS="--workload mycielskian16 --K 512 --alpha 0.5 --delta 0.5" ;;
     M16k64) ARGS="--workload mycielskian16 --K 64 --alpha 0.3 --delta 0.1" ;;
+    M15k128) ARGS="--workload mycielskian15 --K 128 --alpha 0.7 --delta 0.3" ;;
     T128) ARGS="--workload Trefethen_20000 --K 128 --alpha 0.7 --delta 0.5" ;;
     *) echo "unknown config $CFG" >&2; exit 2 ;;
 esac
