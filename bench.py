@@ -7,7 +7,9 @@ the plan of the C2 workload of BASELINE.json: nips-like 1,500 x 12,419 pattern w
 Reordering runs once before timing and is reported separately (the reference's GFLOP/s excludes it
 too, Logger.hpp:178-180). Inputs are resident in HBM when the timed region starts.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): S sharded by
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N, or plain
+`bench.py --gpus N`, which starts that launcher as a child process; a WORLD_SIZE other than
+--gpus is an error, so the line's n_gpus is always --gpus): S sharded by
 row panels (bsmr/dist.py); B is broadcast once from rank 0 over RCCL (xGMI), each
 rank holds only its rows of A, and after timing P is sum-reduced to rank 0 and checked against the
 product's host SDDMM (checkData rule). C2 (default) is weak scaling: the global pattern is N
@@ -136,13 +138,16 @@ def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200):
             return statistics.median(last), times, ok
 
 
-def graph_time(launch, steps, dev):
+def graph_time(launch, steps, dev, out=None, reps=3):
     """ms per step of `steps` launches captured into one HIP graph and replayed (one warm-up
-    replay, then one timed replay between HIP events on the replay stream). launch(stream_handle)
-    issues one step on the given stream. A graph replay submits the K kernels without a host call
-    per launch (the MI355X-native form of a launch-bound loop; at ~10 us per C2 step the ctypes +
-    hipLaunchKernel path per step is as long as the kernel). Returns (ms, None), or (None,
-    reason) when capture fails (the caller then keeps the stream-launched time)."""
+    replay, then `reps` timed replays, each between HIP events on the replay stream; the median).
+    launch(stream_handle) issues one step on the given stream. A graph replay submits the K
+    kernels without a host call per launch (the MI355X-native form of a launch-bound loop; at
+    ~10 us per C2 step the ctypes + hipLaunchKernel path per step is as long as the kernel).
+    out: the output tensor the steps write; it is zeroed before the timed replays and its value
+    after the first one is returned, so the caller can check that the replayed graph computed
+    the same P. Returns (ms, None, P or None, [ms per replay]), or (None, reason, None, []) when
+    capture fails (the caller then keeps the stream-launched time)."""
     import torch
 
     try:
@@ -154,18 +159,25 @@ def graph_time(launch, steps, dev):
                     launch(gs.cuda_stream)
             g.replay()  # warm-up replay
             gs.synchronize()
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(gs)
-            g.replay()
-            e1.record(gs)
-            gs.synchronize()
-        ms = e0.elapsed_time(e1) / max(steps, 1)
+            if out is not None:
+                out.zero_()
+                gs.synchronize()
+            times, P = [], None
+            for r in range(max(1, reps)):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(gs)
+                g.replay()
+                e1.record(gs)
+                gs.synchronize()
+                times.append(e0.elapsed_time(e1) / max(steps, 1))
+                if r == 0 and out is not None:
+                    P = out.cpu().numpy().copy()
         del g
-        return ms, None
+        return statistics.median(times), None, P, times
     except Exception as e:  # noqa: BLE001 - reported; the stream-launched time stays
         torch.cuda.synchronize()
-        return None, f"{type(e).__name__}: {e}"[:300]
+        return None, f"{type(e).__name__}: {e}"[:300], None, []
 
 
 def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
@@ -491,16 +503,68 @@ def pmc_traffic_inrun(args):
         "seconds": round(time.perf_counter() - t0, 1)}
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args):
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE): start N ranks under
+    torch.distributed.run as a CHILD process — this process never touches HIP, and nothing is
+    exec'd — forward its output and exit with its return code. So `--gpus N` always means N ranks
+    (one per GPU); rank 0 of the child prints the JSON line."""
+    import subprocess
+
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus} must be >= 1", file=sys.stderr)
+        return 2
+    if os.environ.get("BSMR_DIST_BACKEND", "nccl") != "gloo":
+        import torch  # device_count() does not initialise HIP
+
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, BSMR_BENCH_SELF_LAUNCHED="1")
+    print(f"bench.py: launching {args.gpus} rank(s): {' '.join(cmd)}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:  # rank 0's JSON line (and any progress) as it comes
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
 def main():
     args = parse()
     from bsmr import dist as D
+
+    rank, world, local = D.env_rank_world()
+    launched = "WORLD_SIZE" in os.environ
+    if args.config != "C1":
+        if launched and world != args.gpus:
+            # the line's n_gpus must be the --gpus the caller asked for
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
+                  "ranks", file=sys.stderr)
+            return 2
+        if not launched and (args.gpus > 1 or args.force_sharded):
+            return self_launch(args)
+    if os.environ.get("BSMR_BENCH_PROBE") == "1":  # launch-path test: report and stop (no GPU)
+        print(json.dumps({"probe": True, "rank": rank, "world": world, "gpus": args.gpus,
+                          "self_launched": os.environ.get("BSMR_BENCH_SELF_LAUNCHED") == "1"}),
+              flush=True)
+        return 0
     from bsmr import set_default_tuning, tuning_from_env
 
     # launch-layout knobs from BSMR_* variables (A/B runs; the library itself reads no
     # environment), recorded in the line when any is set
     args.tuning = tuning_from_env()
     set_default_tuning(args.tuning)
-    rank, world, local = D.env_rank_world()
     if args.config == "C1":
         return main_c1(args)
     sharded = world > 1 or args.force_sharded
@@ -654,17 +718,30 @@ def main_single(args):
     stream_ms_per_step = ms_per_step
     # the timed steps as one HIP graph (graph_time): the line's value when capture works,
     # the stream-launched time beside it
-    graph_ms, graph_err = (None, "--no-graph") if args.no_graph else graph_time(
-        lambda h: plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=h, dtype=dtype),
-        args.steps, dev)
-    if graph_ms is not None:
-        ms_per_step = graph_ms
+    P_stream = dP.cpu().numpy().copy()
+    graph_ms, graph_err, P_graph, graph_reps = (None, "--no-graph", None, []) if args.no_graph \
+        else graph_time(lambda h: plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+                                             stream=h, dtype=dtype), args.steps, dev, out=dP)
     timing = {"method": "hip_graph" if graph_ms is not None else "stream_launches",
               "graph_ms_per_step": round(graph_ms, 5) if graph_ms is not None else None,
+              "graph_replays_ms_per_step": [round(x, 5) for x in graph_reps],
               "stream_launch_ms_per_step": round(stream_ms_per_step, 5),
               "note": "value = the K timed steps captured into one HIP graph and replayed "
-                      "between HIP events (each step a full SDDMM launch); stream_launch = the "
-                      "same K steps launched one by one from Python"}
+                      "between HIP events (each step a full SDDMM launch; the median of 3 timed "
+                      "replays); stream_launch = the same K steps launched one by one from Python"}
+    if P_graph is not None:
+        # P was zeroed before the timed replays: the replayed graph must have written every
+        # output, bit-identical to the stream-launched steps (same kernel, same inputs)
+        import numpy as np
+
+        mism = int(np.count_nonzero(P_graph.view(np.uint32) != P_stream.view(np.uint32)))
+        timing["graph_P_mismatches_vs_stream"] = mism
+        if mism:
+            timing["graph_error"] = f"replayed graph P differs from the stream-launched P in {mism} entries"
+            graph_ms = None
+            timing["method"] = "stream_launches"
+    if graph_ms is not None:
+        ms_per_step = graph_ms
     if graph_err:
         timing["graph_error"] = graph_err
 
@@ -816,7 +893,7 @@ def _timed_steps(step, steps, warmup, stream, use_graph=True, has_work=True):
     if use_graph:
         dist.barrier()
         torch.cuda.synchronize()
-        ms, _ = graph_time(step, steps, stream.device) if has_work else (0.0, None)
+        ms = graph_time(step, steps, stream.device)[0] if has_work else 0.0
         torch.cuda.synchronize()
         # the same method on every rank (the barriers below must pair up)
         if min(D.all_values(1.0 if ms is not None else 0.0, stream.device)) > 0:
@@ -1233,4 +1310,5 @@ def main_sharded(args, rank, world):
 
 
 if __name__ == "__main__":
-    main()
+    rc = main()
+    sys.exit(rc if isinstance(rc, int) else 0)

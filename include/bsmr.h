@@ -22,12 +22,14 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 9  /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 10 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
                               the plan options (no environment reads in the library);
                               7: bsmr_tuning.out_packed; 8: bsmr_tuning.sweep*, rb_sweep;
-                              9: bsmr_tuning.cluster_filter, filter stats */
+                              9: bsmr_tuning.cluster_filter, filter stats;
+                              10: bsmr_plan_check, bsmr_check_rphm_arrays, BSMR_ERR_CHECK,
+                              bsmr_tuning.pair_min_items, stats rb_pairs */
 
 typedef enum {
     BSMR_OK = 0,
@@ -36,7 +38,8 @@ typedef enum {
     BSMR_ERR_REJECTED = 3,    /* matrix rejected by the reference loader rules */
     BSMR_ERR_HIP = 4,         /* HIP runtime error (message via bsmr_last_error) */
     BSMR_ERR_TIMEOUT = 5,     /* a persistent reorder kernel gave up waiting (never expected) */
-    BSMR_ERR_UNSUPPORTED = 6  /* e.g. K not a multiple of 16, dtype not built */
+    BSMR_ERR_UNSUPPORTED = 6, /* e.g. K not a multiple of 16, dtype not built */
+    BSMR_ERR_CHECK = 7        /* bsmr_plan_check found a structural error (bsmr_last_error) */
 } bsmr_status;
 
 typedef enum { BSMR_F32 = 0, BSMR_F16 = 1, BSMR_BF16 = 2 } bsmr_dtype;
@@ -142,6 +145,10 @@ typedef struct {
                                   reach alpha (same permutation), 0 never, 1 when
                                   alpha >= 0.01 and its buffers fit a quarter of the free memory,
                                   -1 = auto (the same, from 32768 rows) */
+    int32_t pair_min_items;    /* BSMR_PAIR_MIN_ITEMS: staged-output row-block layouts of rows >= 512 B
+                                  with at least this many list items run two items per workgroup
+                                  (k_sddmm_rb_pair, the second item's staging under the first's
+                                  stores); -1 = 4096 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -242,6 +249,8 @@ typedef struct {
      * (included in row_reorder_ms) */
     uint32_t cluster_filter_used;
     float cluster_filter_ms;
+    /* bit i set: row-block layout i (as rb_rows) launches two items per workgroup (pairs) */
+    uint32_t rb_pairs;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);
@@ -276,6 +285,35 @@ typedef struct {
     int32_t num_sparse_data;          /* bsmr_numSparseData */
 } bsmr_eval_stats;
 int bsmr_plan_evaluate(const bsmr_plan* plan, bsmr_eval_stats* out);
+
+/* Replaces check_rphm(matrix, bsmr, rphm, delta) (src/BSMR.cpp:932-953, with check_rowReordering
+ * 444-486, check_colReordering 488-637 and check_rphm 639-824), which the reference runs under
+ * VALIDATE before checkSddmm (src/sddmm.cu:34-38). Host check of the plan against its S:
+ *   row reordering: every non-empty row exactly once, no empty row;
+ *   column reordering: per panel the dense / sparse column lists are the panel's columns, each
+ *     once, in descending count order, padded with the sentinel N, the dense prefix exactly the
+ *     16-column groups reaching ceil(delta * 256) entries, the sparse data in order and counted;
+ *   RPHM: every blockValues slot the CSR index of its (row, column) or NULL, every sparse value in
+ *     its row and column, every stored entry in exactly one of blockValues / sparseValues;
+ *   launch layout (K > 0): the layout bsmr_sddmm runs for (K, dtype) computes every stored entry
+ *     exactly once (kept MFMA tile, column-run piece or residual slot) with its row, column and
+ *     output position consistent with S.
+ * verbose != 0 prints the reference's messages on stderr ("Error! Row is duplicated! ...", then
+ * "Error! The row reordering is incorrect!" / "... col reordering ..." / "... rphm ..." / "Error!
+ * The launch layout is incorrect! ..."). Returns BSMR_OK when every check passes, BSMR_ERR_CHECK
+ * when one fails (bsmr_last_error names the first failure). Not timed; O(nnz) host work. */
+int bsmr_plan_check(const bsmr_plan* plan, uint32_t K, int dtype, int verbose);
+/* The same row / column / RPHM checks over caller host arrays (S in CSR, and the plan arrays as
+ * bsmr_plan_get_array returns them: R reordered rows, P = ceil(R / 16) panels), e.g. a plan dumped
+ * by another build or the reference's own RPHM copied to the host. No device needed. */
+int bsmr_check_rphm_arrays(uint32_t M, uint32_t N, uint32_t nnz, const uint32_t* rowptr,
+                           const uint32_t* colidx, uint32_t R, const uint32_t* rows,
+                           const uint32_t* denseColOffsets, const uint32_t* denseCols,
+                           const uint32_t* sparseColOffsets, const uint32_t* sparseCols,
+                           const uint32_t* sparseValueOffsets, const uint32_t* blockOffsets,
+                           const uint32_t* blockValues, const uint32_t* sparseValues,
+                           const uint32_t* sparseRelativeRows, const uint32_t* sparseColIndices,
+                           float delta, int verbose);
 
 /* ------------------------------------------------------------------------- SDDMM ---- */
 /* Replaces sddmm_gpu(M, N, K, dA, dB, rphm, dP, logger) (include/sddmmKernel.cuh:25-30,

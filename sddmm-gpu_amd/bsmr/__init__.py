@@ -21,6 +21,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("BSMR_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libbsmr_amd.so")
 
 F32, F16, BF16 = 0, 1, 2
+CHECK_FAILED = 7  # BSMR_ERR_CHECK
 
 ARRAYS = {
     "reorderedRows": 0, "denseCols": 1, "denseColOffsets": 2, "sparseCols": 3,
@@ -48,7 +49,7 @@ class Tuning(C.Structure):
                 ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
                 ("item_sched", C.c_int32), ("out_packed", C.c_int32), ("sweep", C.c_int32),
                 ("sweep_range_kb", C.c_int32), ("sweep_split", C.c_float), ("sweep_slack", C.c_int32),
-                ("cluster_filter", C.c_int32)]
+                ("cluster_filter", C.c_int32), ("pair_min_items", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -81,7 +82,7 @@ class PlanStats(C.Structure):
                 ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5),
                 ("dense_sampled_tiles", C.c_uint32), ("rb_orig_rows", C.c_uint32),
                 ("rb_sweep", C.c_uint32), ("cluster_filter_used", C.c_uint32),
-                ("cluster_filter_ms", C.c_float)]
+                ("cluster_filter_ms", C.c_float), ("rb_pairs", C.c_uint32)]
 
     def as_dict(self):
         d = {}
@@ -121,7 +122,7 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 9  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 10  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -136,6 +137,7 @@ EXPORTS = [
     "bsmr_sddmm_panels_local",
     "bsmr_plan_export_rows", "bsmr_plan_import_rows",
     "bsmr_sddmm_profile", "bsmr_sddmm_cpu", "bsmr_check_one", "bsmr_check_data",
+    "bsmr_plan_check", "bsmr_check_rphm_arrays",
 ]
 
 _lib = None
@@ -210,6 +212,11 @@ def lib():
     L.bsmr_sddmm_profile.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_int, vp,
                                      C.POINTER(C.c_float), C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]
+    L.bsmr_plan_check.argtypes = [vp, C.c_uint32, C.c_int, C.c_int]
+    L.bsmr_plan_check.restype = C.c_int
+    L.bsmr_check_rphm_arrays.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32] + [_u32p] * 2 + \
+        [C.c_uint32] + [_u32p] * 11 + [C.c_float, C.c_int]
+    L.bsmr_check_rphm_arrays.restype = C.c_int
     _lib = L
     return L
 
@@ -415,6 +422,17 @@ class Plan:
         _check(lib().bsmr_plan_evaluate(self.h, C.byref(e)), "bsmr_plan_evaluate")
         return e.as_dict()
 
+    def check(self, K=0, dtype=F32, verbose=True):
+        """bsmr_plan_check (the reference's check_rphm, BSMR.cpp:932-953): (True, "") when the plan
+        and, for K > 0, the launch layout of (K, dtype) pass; (False, first error) otherwise."""
+        st = lib().bsmr_plan_check(self.h, K, dtype, 1 if verbose else 0)
+        if st == 0:
+            return True, ""
+        msg = lib().bsmr_last_error().decode(errors="replace")
+        if st != CHECK_FAILED:
+            raise BsmrError(f"bsmr_plan_check failed with status {st}: {msg}")
+        return False, msg
+
     def sddmm(self, dA, dB, K, dP, stream=0, dtype=F32):
         """dA, dB, dP: device pointers (int) — e.g. torch tensor .data_ptr()."""
         _check(lib().bsmr_sddmm(self.h, dA, dB, K, dtype, dP, stream or None), "bsmr_sddmm")
@@ -483,6 +501,26 @@ def sddmm_cpu(M, N, rowptr, colidx, K, A, B, threads=0):
     _check(lib().bsmr_sddmm_cpu(rowptr, colidx, M, N, K, np.ascontiguousarray(A, np.float32),
                                 np.ascontiguousarray(B, np.float32), P, threads), "bsmr_sddmm_cpu")
     return P
+
+
+def check_rphm_arrays(M, N, rowptr, colidx, arrays, delta, verbose=True):
+    """bsmr_check_rphm_arrays: the reference's check_rphm (BSMR.cpp:932-953) over host arrays.
+    `arrays` maps the plan array names (ARRAYS keys) to uint32 arrays. Returns (ok, first error)."""
+    a = {k: np.ascontiguousarray(v, dtype=np.uint32) for k, v in arrays.items()}
+    rp = np.ascontiguousarray(rowptr, dtype=np.uint32)
+    ci = np.ascontiguousarray(colidx, dtype=np.uint32)
+    order = ["denseColOffsets", "denseCols", "sparseColOffsets", "sparseCols",
+             "sparseValueOffsets", "blockOffsets", "blockValues", "sparseValues",
+             "sparseRelativeRows", "sparseColIndices"]
+    rows = a["reorderedRows"]
+    st = lib().bsmr_check_rphm_arrays(M, N, len(ci), rp, ci, len(rows), rows,
+                                      *[a[k] for k in order], float(delta), 1 if verbose else 0)
+    if st == 0:
+        return True, ""
+    msg = lib().bsmr_last_error().decode(errors="replace")
+    if st != CHECK_FAILED:
+        raise BsmrError(f"bsmr_check_rphm_arrays failed with status {st}: {msg}")
+    return False, msg
 
 
 def check_data(data1, data2, verbose=False):

@@ -39,6 +39,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->sweep = t->sweep_range_kb = t->sweep_slack = -1;
     t->sweep_split = -1.0f;
     t->cluster_filter = -1;
+    t->pair_min_items = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -91,6 +92,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     getf("BSMR_SWEEP_SPLIT", t->sweep_split);
     geti("BSMR_SWEEP_SLACK", t->sweep_slack);
     get3("BSMR_CLUSTER_FILTER", t->cluster_filter);
+    geti("BSMR_PAIR_MIN_ITEMS", t->pair_min_items);
     return n;
 }
 
@@ -150,6 +152,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->sweep_split >= 0) p.sweep_split = std::max(0.25f, t->sweep_split);
         if (t->sweep_slack >= 0) p.sweep_slack = static_cast<u32>(t->sweep_slack);
         if (t->cluster_filter >= 0) p.cluster_filter = t->cluster_filter ? 1 : 0;
+        if (t->pair_min_items >= 0) p.pair_min_items = static_cast<u32>(t->pair_min_items);
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -368,6 +371,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
         if (L.rowBytes && L.orig) s->rb_orig_rows |= 1u << i;
         if (L.rowBytes && L.sweep) s->rb_sweep |= 1u << i;
+        if (L.rowBytes && rb_uses_pairs(p, L)) s->rb_pairs |= 1u << i;
     }
     s->dense_sampled_tiles = p.dense.built ? p.dense.nonempty : 0;
     return BSMR_OK;

@@ -121,6 +121,33 @@ bool check_sddmm(const bsmr_csr* S, uint32_t K, const Operands& ops, std::vector
     return true;
 }
 
+#ifdef BSMR_FAULT_INJECT
+// test hook of the library (not in the header): one plan / layout array element overwritten
+extern "C" int bsmr_debug_plan_poke(bsmr_plan* plan, int which, uint64_t index, uint32_t value,
+                                    uint32_t K, int dtype, uint32_t* old);
+#endif
+
+// check_rphm (sddmm.cu:36, BSMR.cpp:932-953): the plan's structural self-check, then the launch
+// layout of this K; messages on stderr as the reference prints them. Fault injection (test build
+// only): BSMR_VALIDATE_CORRUPT_PLAN="which:index:value" overwrites one array element first
+// (which: a bsmr_array value, 100/101 the row-block layout's entries / pieces).
+bool check_plan(bsmr_plan* plan, uint32_t K) {
+#ifdef BSMR_FAULT_INJECT
+    if (const char* c = std::getenv("BSMR_VALIDATE_CORRUPT_PLAN")) {
+        unsigned which = 0, value = 0;
+        unsigned long long index = 0;
+        if (std::sscanf(c, "%u:%llu:%u", &which, &index, &value) == 3) {
+            uint32_t old = 0;
+            const int st = bsmr_debug_plan_poke(plan, static_cast<int>(which), index, value, K, BSMR_F32, &old);
+            if (st) die("bsmr_debug_plan_poke", st);
+        }
+    }
+#endif
+    const int st = bsmr_plan_check(plan, K, BSMR_F32, 1);
+    if (st != BSMR_OK && st != BSMR_ERR_CHECK) die("bsmr_plan_check", st);
+    return st == BSMR_OK;
+}
+
 bool validate_enabled() {
     const char* v = std::getenv("BSMR_VALIDATE");
     return v && v[0] && v[0] != '0';
@@ -244,6 +271,7 @@ int main(int argc, char* argv[]) {
         std::vector<float> P;
         Operands ops;
         run_sddmm(plan, S, K, options.numIterations(), log, &P, &ops);
+        check_plan(plan, K);        // check_rphm, then checkSddmm (sddmm.cu:35-37)
         check_sddmm(S, K, ops, P);  // printed before the log block, as sddmm() does
     } else {
         run_sddmm(plan, S, K, options.numIterations(), log, nullptr);

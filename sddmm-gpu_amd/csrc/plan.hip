@@ -1766,23 +1766,29 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         // column weight: its entries, plus (item_sched) piece_weight per column-run piece it
         // heads, so the XCDs' ranges carry equal modeled cost rather than equal entry counts
         // (mycielskian: the last XCD's range carried 10 % more piece work and ended 10 % later)
-        // (per-thread sums over row blocks, added in thread order: with the default integral
-        // weights every partial sum is exact, so the cuts do not depend on the split)
-        std::vector<std::vector<double>> cntT(16);
-        par_for(nRB, [&](unsigned t, size_t b0, size_t b1) {
-            std::vector<double>& cnt = cntT[t];
-            cnt.assign(N + 1, 0.0);
-            for (size_t b = b0; b < b1; ++b) {
-                const u32 lo = b ? std::max(rbEnd[b - 1], 0u) : 0u, hi = rbEnd[b];
-                u32 run = 0;
-                for (u32 i = lo; i < hi; ++i) {
-                    const u32 c = hmeta[i] & CM;
-                    const bool start = i == lo || c != (hmeta[i - 1] & CM) || run >= piece_max;
-                    run = start ? 1 : run + 1;
-                    cnt[c] += 1.0 + (item_cost_cuts && start ? piece_weight : 0.0);
+        // (sums over 16 fixed chunks of row blocks, whatever the host's thread count, added in
+        // chunk order: the cuts are the same on every host even for a non-integral piece_weight,
+        // so every rank of a multi-GPU run derives the same layout)
+        constexpr u32 NCH = 16;
+        std::vector<std::vector<double>> cntT(NCH);
+        par_for(NCH, [&](unsigned, size_t c0, size_t c1) {
+            for (size_t ch = c0; ch < c1; ++ch) {
+                std::vector<double>& cnt = cntT[ch];
+                const size_t b0 = static_cast<size_t>(nRB) * ch / NCH, b1 = static_cast<size_t>(nRB) * (ch + 1) / NCH;
+                if (b0 == b1) continue;
+                cnt.assign(N + 1, 0.0);
+                for (size_t b = b0; b < b1; ++b) {
+                    const u32 lo = b ? std::max(rbEnd[b - 1], 0u) : 0u, hi = rbEnd[b];
+                    u32 run = 0;
+                    for (u32 i = lo; i < hi; ++i) {
+                        const u32 c = hmeta[i] & CM;
+                        const bool start = i == lo || c != (hmeta[i - 1] & CM) || run >= piece_max;
+                        run = start ? 1 : run + 1;
+                        cnt[c] += 1.0 + (item_cost_cuts && start ? piece_weight : 0.0);
+                    }
                 }
             }
-        }, 16);
+        }, 1);
         std::vector<double> cnt(N + 1, 0.0);
         for (const auto& ct : cntT)
             if (!ct.empty())
@@ -2326,36 +2332,38 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             BSMR_HIP(hipMemcpyAsync(hpos.data(), L.sortedPos.data(), n * sizeof(u32),
                                     hipMemcpyDeviceToHost, s));
             BSMR_HIP(hipStreamSynchronize(s));
-            // (per item on the host threads, then placed in item order)
-            std::vector<std::vector<uint2>> ir(ient.size());
-            std::vector<char> over(ient.size(), 0);
-            par_for(ient.size(), [&](unsigned, size_t i0, size_t i1) {
-                for (size_t i = i0; i < i1; ++i) {
-                    const u32 e0 = ient[i].x, len = ient[i].y;
-                    for (u32 t = 0; t < len;) {
-                        // a run is one wave store: at most 64 consecutive positions (an unsplit
-                        // original-order item is one long run, which would leave all but one
-                        // wave idle in the store pass)
-                        u32 u = t + 1;
-                        while (u < len && u - t < 64 && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
-                        ir[i].push_back(make_uint2(hpos[e0 + t], t | ((u - t) << 16)));
-                        t = u;
-                    }
-                    over[i] = ir[i].size() > NT;
+            // two passes on the host threads: count each item's runs, then (offsets by a scan)
+            // write them in item order into one flat table (no per-item vectors: C4 x1 holds
+            // ~60 M runs)
+            // a run is one wave store: at most 64 consecutive positions (an unsplit original-order
+            // item is one long run, which would leave all but one wave idle in the store pass)
+            auto runs_of = [&](size_t i, uint2* dst) {
+                const u32 e0 = ient[i].x, len = ient[i].y;
+                u32 nrun = 0;
+                for (u32 t = 0; t < len;) {
+                    u32 u = t + 1;
+                    while (u < len && u - t < 64 && hpos[e0 + u] == hpos[e0 + u - 1] + 1) ++u;
+                    if (dst) dst[nrun] = make_uint2(hpos[e0 + t], t | ((u - t) << 16));
+                    ++nrun;
+                    t = u;
                 }
+                return nrun;
+            };
+            std::vector<uint2> hir(ient.size(), make_uint2(0, 0));
+            par_for(ient.size(), [&](unsigned, size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i) hir[i].y = runs_of(i, nullptr);
             });
             bool fits = true;
-            std::vector<uint2> hir(ient.size(), make_uint2(0, 0));
             size_t nr = 0;
             for (size_t i = 0; i < ient.size(); ++i) {
-                fits = fits && !over[i];
-                hir[i] = make_uint2(static_cast<u32>(nr), static_cast<u32>(ir[i].size()));
-                nr += ir[i].size();
+                fits = fits && hir[i].y <= NT;
+                hir[i].x = static_cast<u32>(nr);
+                nr += hir[i].y;
             }
             std::vector<uint2> hr(fits ? nr : 0);
             if (fits)
                 par_for(ient.size(), [&](unsigned, size_t i0, size_t i1) {
-                    for (size_t i = i0; i < i1; ++i) std::copy(ir[i].begin(), ir[i].end(), hr.begin() + hir[i].x);
+                    for (size_t i = i0; i < i1; ++i) runs_of(i, hr.data() + hir[i].x);
                 });
             if (fits) {
                 BSMR_CHECK(L.runs.upload(hr.data(), std::max<size_t>(hr.size(), 1), s));

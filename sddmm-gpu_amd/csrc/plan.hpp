@@ -117,6 +117,9 @@ struct Plan {
     int cluster_filter = -1;
     u32 filter_min_rows = 32768;
     bool filter_used = false;
+    // staged-output row-block layouts (rows >= 512 B) of at least this many items run in pairs
+    // (k_sddmm_rb_pair; bsmr_tuning.pair_min_items)
+    u32 pair_min_items = 4096;
     float filter_ms = 0.f;
 
     // input
@@ -280,6 +283,8 @@ struct Plan {
 
 // the whole plan's row-block layout for (K, dtype) (sddmm.hip); *out = null for column-major
 int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out);
+// whether a full launch of layout L runs two items per workgroup (k_sddmm_rb_pair; sddmm.hip)
+bool rb_uses_pairs(const Plan& p, const Plan::RowBlockLayout& L);
 
 }  // namespace bsmr
 

@@ -1528,12 +1528,11 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     // 56.9 / 74.6 us paired against 50.1 / 66.5 unpaired, mycielskian16 K = 64 114.6 against
     // 108.9; C4 (8-30 K items) gains (x0.5 1.029 -> 0.984 ms), C3, mycielskian16 K = 128 and
     // 1-2 KiB rows are neutral (profiles/r04zt, r04zw)
-    a.pairs = mode == 3 && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= 4096 && L.nTilesKept == 0 &&
-                      L.nItems % (2 * XCD_BUCKETS) == 0 && !a.stageNt && a.lateB &&
-                      !(p.diag & (8u | 32u | 64u | 128u | 16384u))
-                  ? 1u
-                  : 0u;
-    if (L.sweep) {
+    a.pairs = mode == 3 && rb_uses_pairs(p, L) ? 1u : 0u;
+    // the range sweep's per-XCD step counters serve one launch of one batch: batched launches run
+    // a sweep layout's items as independent workgroups on k_sddmm_rb (items are self-contained)
+    const bool sweep = L.sweep && nb == 1;
+    if (sweep) {
         a.pairs = 0;
         a.wgStart = L.wgStart.data();
         a.itemStep = L.itemStep.data();
@@ -1557,7 +1556,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, L.sweep)
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, sweep)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
@@ -1572,7 +1571,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
 #undef BSMR_RB2
 #undef BSMR_RB
     // k_sddmm_rb stages a fixed 160 / 80 KiB per workgroup (the image and an unused tail)
-    const u32 grid = L.sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
+    const u32 grid = sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
     hipLaunchKernelGGL(fn, dim3(grid, nb), dim3(L.NT),
                        (L.NT == 1024 ? 160 : 80) * 1024, s, a);
     BSMR_HIP(hipGetLastError());
@@ -1604,6 +1603,20 @@ int launch_panels(SddmmArgs a, hipStream_t s) {
 }
 
 }  // namespace
+
+// pairs (BSMR_DIAG & 16384 off): staged output by runs, rows of >= 512 bytes, at least
+// pair_min_items (4096: 16 rounds of the chip's workgroup slots) items, an even number of list
+// positions per XCD, no kept MFMA tile; not under the profiling ablations (trace, staging only, B
+// in L2, no stores) nor nt staging / early B loads
+bool rb_uses_pairs(const Plan& p, const Plan::RowBlockLayout& L) {
+    const bool stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
+    return !L.sweep && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= p.pair_min_items &&
+           L.nTilesKept == 0 && L.nItems % (2 * XCD_BUCKETS) == 0 && !stageNt && p.late_b != 0 &&
+           !(p.diag & (8u | 32u | 64u | 128u | 16384u));
+}
+
+// whether bsmr_sddmm runs the dense-sampled launch for (K, dtype) (plan_check.cpp)
+bool sddmm_uses_dense(const Plan& p, u32 K, int dtype) { return use_dense(p, K, dtype); }
 
 // the whole plan's row-block layout for (K, dtype), built on first use; *out = null when that
 // (K, dtype) runs the column-major launch

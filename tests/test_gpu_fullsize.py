@@ -11,6 +11,7 @@ HIP SDDMM against the oracle's host SDDMM (host.cpp:45-76 loop order) by the che
   original row panels of equal stored entries, each with its own plan);
 * C5 DLMC-like 2048^2 90 %-sparse masks (uniform: the dense-sampled MFMA launch; 16x16 blocks: the
   column-major tile launch), bf16, K = 512.
+Each plan also passes bsmr_plan_check (check_rphm + its launch layout) at that size.
 """
 import functools
 
@@ -70,6 +71,10 @@ def test_full_workload_every_entry(name, K, dtype):
     assert np.isfinite(P).all()
     assert O.check_data(ref, P) == 0
     del P
+    # the reference's structural self-check (check_rphm, BSMR.cpp:932-953) and the launch layout
+    # of (K, dtype): every stored entry computed exactly once, at the full size
+    ok, msg = plan.check(K, dtype)
+    assert ok, msg
     if name == "C4":  # the north_star split: 8 row-panel shards, each with only its A rows
         rows = plan.array("reorderedRows")
         shards = [plan.shard(K, r, 8, dtype) for r in range(8)]

@@ -223,6 +223,29 @@ def test_bench_sharded_rccl_one_rank():
     assert sum(sc["global"]["shards"]["entries"]) == sc["nnz"]
 
 
+@pytest.mark.timeout(600)
+def test_bench_self_launch_force_sharded_one_gpu():
+    """`bench.py --gpus 1 --force-sharded` with no launcher: bench starts torch.distributed.run as
+    a child (the same path `--gpus 8` takes on the driver's node) and the line reports the ranks
+    that ran, with the strong_C4 block of the north_star split."""
+    env = dict(os.environ, OMP_NUM_THREADS="8")
+    for k in ("BSMR_DIST_BACKEND", "WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--force-sharded",
+           "--steps", "5", "--warmup", "2", "--strong", "on", "--strong-scale", "0.05",
+           "--no-vendor", "--pmc", "off"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=540, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "torch.distributed.run" in r.stderr
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 1 and out["config"]["backend"] == "nccl"
+    assert out["checkData_errors_gathered_P"] == 0
+    for split in ("global", "local"):
+        assert out["strong_C4"][split]["checkData_errors_gathered_P"] == 0, split
+
+
 def test_shard_rebalance_moves_cuts_toward_measured_balance():
     """bsmr_plan_shard_rebalance: cuts stay on row-block boundaries, span [0, P], do not move
     when every shard took the same time per model cost, and shrink a shard that ran slow."""

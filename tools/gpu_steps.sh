@@ -21,6 +21,10 @@
 #                           in turn (permutation hash and clustering ms per run)
 #   ablib:<variant.so>:cfg1,cfg2[:swap]   tools/ab_lib.sh: the in-tree library against a variant
 #                           build (swap: the variant runs first in each pair)
+#   guard                   tools/perf_guard.py --check profiles/perf_baseline.json: the 20
+#                           published SuiteSparse points + C2-C5 against the committed baseline,
+#                           rc 1 on any > 5 % loss (run after every layout-rule commit)
+#   guard:record            the same points written as a new baseline (gpurun_out/<tag>/)
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -76,6 +80,12 @@ run_step() {
                 BSMR_DIAG=$d timeout -k 10 300 python3 tools/plan_time.py --workload reddit_like --scale "$scale" --batches 16384 > "$OUT/plan_${scale}_$d.json" 2>> "$OUT/$f.log" || return $?
                 python3 -c "import json; d=json.load(open('$OUT/plan_${scale}_$d.json')); r=list(d['runs'].values())[0]; print('scale $scale diag $d', r['row_reorder_ms'], r['rows_sha256'], r['num_clusters'], r['wall_s'])" >> "$OUT/planab_summary.txt"
             done ;;
+        guard)
+            if [ "$arg" = "record" ]; then
+                timeout -k 10 900 python3 -u tools/perf_guard.py --record "$OUT/perf_baseline.json" > "$OUT/guard_record.log" 2>&1
+            else
+                timeout -k 10 900 python3 -u tools/perf_guard.py --check profiles/perf_baseline.json --out "$OUT/guard.json" > "$OUT/guard.log" 2>&1
+            fi ;;
         *) echo "unknown step $s" >&2; return 2 ;;
     esac
     local rc=$?
