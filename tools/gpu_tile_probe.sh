@@ -12,3 +12,6 @@ SETS=${*:-"- TILE_MIN_F32=0 TILE_MIN_F32=128 TILE_MIN_F32=192"}
 bash tools/ab_grid.sh "$TAG" C2 $SETS || exit $?
 timeout -k 10 300 python3 tools/trace_sddmm.py --workload nips_like --K 128 > "$OUT/trace_default.json" 2> "$OUT/trace_default.err" || exit $?
 BSMR_TILE_MIN_F32=0 timeout -k 10 300 python3 tools/trace_sddmm.py --workload nips_like --K 128 > "$OUT/trace_tiles.json" 2> "$OUT/trace_tiles.err" || exit $?
+for t in 257 0 128 192; do
+    BSMR_TILE_MIN_F32=$t timeout -k 10 120 python3 tools/tile_items.py > "$OUT/items_$t.json" 2>> "$OUT/items.err" || exit $?
+done
