@@ -15,6 +15,12 @@ for c in $CFGS; do
         C4x1) ARGS="--workload reddit_like --scale 1.0 --K 128 --dtype f32" ;;
         C5u) ARGS="--workload dlmc_like --mask uniform --K 512 --dtype bf16" ;;
         C5b) ARGS="--workload dlmc_like --mask block --K 512 --dtype bf16" ;;
+        C2k32) ARGS="--workload nips_like --K 32 --dtype f32" ;;
+        C2k512) ARGS="--workload nips_like --K 512 --dtype f32" ;;
+        M15k32) ARGS="--workload mycielskian15 --K 32 --alpha 0.9 --delta 0.1" ;;
+        M15k64) ARGS="--workload mycielskian15 --K 64 --alpha 0.3 --delta 0.1" ;;
+        M14k256) ARGS="--workload mycielskian14 --K 256 --alpha 0.7 --delta 0.7" ;;
+        M16k32) ARGS="--workload mycielskian16 --K 32 --alpha 0.3 --delta 0.1" ;;
     esac
     for v in $ORDER; do
         if [ $v = var ]; then export BSMR_LIB_PATH=$VAR; else unset BSMR_LIB_PATH; fi

@@ -21,6 +21,9 @@
 #                           in turn (permutation hash and clustering ms per run)
 #   ablib:<variant.so>:cfg1,cfg2[:swap]   tools/ab_lib.sh: the in-tree library against a variant
 #                           build (swap: the variant runs first in each pair)
+#   driverprof              rocprofv3 --kernel-trace --stats of exactly the driver's BENCH command
+#                           (bench.py --gpus 1 --steps 20 --warmup 5; --pmc off: the in-run PMC
+#                           children would run under the tracer too) + tools/rocprof_runs.py
 #   guard                   tools/perf_guard.py --check profiles/perf_baseline.json: the 20
 #                           published SuiteSparse points + C2-C5 against the committed baseline,
 #                           rc 1 on any > 5 % loss (run after every layout-rule commit)
@@ -80,6 +83,9 @@ run_step() {
                 BSMR_DIAG=$d timeout -k 10 300 python3 tools/plan_time.py --workload reddit_like --scale "$scale" --batches 16384 > "$OUT/plan_${scale}_$d.json" 2>> "$OUT/$f.log" || return $?
                 python3 -c "import json; d=json.load(open('$OUT/plan_${scale}_$d.json')); r=list(d['runs'].values())[0]; print('scale $scale diag $d', r['row_reorder_ms'], r['rows_sha256'], r['num_clusters'], r['wall_s'])" >> "$OUT/planab_summary.txt"
             done ;;
+        driverprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_driver" -o run -- \
+                     python3 bench.py --gpus 1 --steps 20 --warmup 5 --pmc off > "$OUT/driverprof.json" 2> "$OUT/driverprof.err" &&
+                   python3 tools/rocprof_runs.py "$(ls "$OUT"/prof_driver/*/run_kernel_trace.csv "$OUT"/prof_driver/run_kernel_trace.csv 2>/dev/null | head -1)" > "$OUT/driverprof_runs.json" ;;
         guard)
             if [ "$arg" = "record" ]; then
                 timeout -k 10 900 python3 -u tools/perf_guard.py --record "$OUT/perf_baseline.json" > "$OUT/guard_record.log" 2>&1

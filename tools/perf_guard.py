@@ -7,7 +7,8 @@ mycielskian14/15/16 at K = 32, 64, 128, 256; each at the (alpha, delta) its test
 best, rows 7 / 350 / 363 / 367 / 444 of scripts/results_suiteSparse_dataset/k*/results_*.csv) and
 the bench configs C2 (K = 32 / 128 / 512), C3, C4 x0.5, C4 x1, C5 uniform / block — and compares
 them with a committed baseline (profiles/perf_baseline.json). Any point more than --tol (5 %)
-slower fails the run (exit 1), so a layout rule fitted on a few matrices cannot silently slow a
+slower than the run's median slowdown (the box factor: boxes differ by a few percent), or a box
+factor itself above --tol, fails the run (exit 1), so a layout rule fitted on a few matrices cannot silently slow a
 published point again (round 4: the pair / range rules took mycielskian15 K = 64 from 16.1 to
 12.6 TFLOP/s and were found only by a manual refresh).
 
@@ -134,11 +135,19 @@ def main():
             worst = max(worst, slow)
             line += f"   baseline {b * 1e3:10.2f} us  {slow * 100:+6.1f} %"
             if slow > args.tol:
-                fails.append(p["name"])
-                line += "  SLOWER"
+                line += "  slower"
         print(line, flush=True)
         res[p["name"]] = dict(p, **r)
-    out = {"tuning": tuning, "tol": args.tol, "points": res,
+    # box factor: the median slowdown over all points. A whole box runs a few percent faster or
+    # slower than the one that recorded the baseline (r05i: +1 %, mycielskian points +2..5 %); a
+    # point fails when it is more than tol slower than the box factor, and the run fails when the
+    # box factor itself exceeds tol (a regression of every point)
+    slows = [r["vs_baseline"] for r in res.values() if "vs_baseline" in r]
+    box = statistics.median(slows) if slows else 0.0
+    fails = [n for n, r in res.items() if "vs_baseline" in r and r["vs_baseline"] - max(box, 0.0) > args.tol]
+    if slows and box > args.tol:
+        fails.append("box_factor")
+    out = {"tuning": tuning, "tol": args.tol, "points": res, "box_factor": round(box, 4),
            "worst_slowdown": round(worst, 4), "failed": fails}
     if args.record:
         with open(args.record, "w") as f:
@@ -148,7 +157,8 @@ def main():
             json.dump(out, f, indent=1)
     if args.check:
         print(json.dumps({"guard": "FAIL" if fails else "PASS", "failed": fails,
-                          "worst_slowdown": round(worst, 4), "tuning": tuning}))
+                          "box_factor": round(box, 4), "worst_slowdown": round(worst, 4),
+                          "tuning": tuning}))
         return 1 if fails else 0
     return 0
 
