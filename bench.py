@@ -138,15 +138,18 @@ def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200):
             return statistics.median(last), times, ok
 
 
+GRAPH_LEAD_CYCLES = 200_000  # torch.cuda._sleep spin ahead of each timed replay (~0.1 ms)
+
+
 def graph_time(launch, steps, dev, out=None, reps=3):
     """ms per step of `steps` launches captured into one HIP graph and replayed (one warm-up
     replay, then `reps` timed replays, each between HIP events on the replay stream; the median).
     launch(stream_handle) issues one step on the given stream. A graph replay submits the K
     kernels without a host call per launch (the MI355X-native form of a launch-bound loop; at
     ~10 us per C2 step the ctypes + hipLaunchKernel path per step is as long as the kernel).
-    out: the output tensor the steps write; it is zeroed before the timed replays and its value
-    after the first one is returned, so the caller can check that the replayed graph computed
-    the same P. Returns (ms, None, P or None, [ms per replay]), or (None, reason, None, []) when
+    out: the output tensor the steps write; it is zeroed after the warm-up replay, one more
+    untimed replay fills it, and that P is returned, so the caller can check that the replayed
+    graph computed the same P. Returns (ms, None, P or None, [ms per replay]), or (None, reason, None, []) when
     capture fails (the caller then keeps the stream-launched time)."""
     import torch
 
@@ -159,20 +162,29 @@ def graph_time(launch, steps, dev, out=None, reps=3):
                     launch(gs.cuda_stream)
             g.replay()  # warm-up replay
             gs.synchronize()
+            P = None
             if out is not None:
+                # P zeroed, one more (untimed) replay, and its P kept for the caller's check: the
+                # replayed graph must write every output
                 out.zero_()
+                g.replay()
                 gs.synchronize()
-            times, P = [], None
+                P = out.cpu().numpy().copy()
+            times = []
             for r in range(max(1, reps)):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
+                # a short spin kernel queued ahead of the start event keeps the stream busy while
+                # the host submits the event and the graph, so the events bracket the K steps'
+                # device time and not the host's graph-launch latency (≈ 10 µs per replay, 0.5 µs
+                # per step at the driver's 20 steps; rocprofv3 trace of the driver's command,
+                # DESIGN.md §8). The steps themselves are unchanged.
+                torch.cuda._sleep(GRAPH_LEAD_CYCLES)
                 e0.record(gs)
                 g.replay()
                 e1.record(gs)
                 gs.synchronize()
                 times.append(e0.elapsed_time(e1) / max(steps, 1))
-                if r == 0 and out is not None:
-                    P = out.cpu().numpy().copy()
         del g
         return statistics.median(times), None, P, times
     except Exception as e:  # noqa: BLE001 - reported; the stream-launched time stays
@@ -728,7 +740,9 @@ def main_single(args):
               "stream_launch_ms_per_step": round(stream_ms_per_step, 5),
               "note": "value = the K timed steps captured into one HIP graph and replayed "
                       "between HIP events (each step a full SDDMM launch; the median of 3 timed "
-                      "replays); stream_launch = the same K steps launched one by one from Python"}
+                      "replays, each queued behind a short spin kernel so the events bracket the "
+                      "steps' device time, not the host's graph launch); stream_launch = the same "
+                      "K steps launched one by one from Python"}
     if P_graph is not None:
         # P was zeroed before the timed replays: the replayed graph must have written every
         # output, bit-identical to the stream-launched steps (same kernel, same inputs)
