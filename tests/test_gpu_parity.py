@@ -433,6 +433,34 @@ def test_range_sweep_matches_plain_staged(K, dtype):
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-5, atol=1e-5 * np.abs(outs[1]).max())
 
 
+def test_range_sweep_layout_batched():
+    """A range-sweep layout launched for several batches (bsmr_sddmm_batch): the sweep's per-XCD
+    step counters serve one batch, so batched launches run the layout's items on the plain
+    row-block kernel; every batch passes checkData."""
+    torch = torch_cuda()
+    M, N, rp, ci = wide_case()
+    K, nb = 128, 2
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock",
+                tuning=tuning_from_env({"BSMR_OUT_STAGED": "1", "BSMR_SWEEP": "1",
+                                        "BSMR_SWEEP_RANGE_KB": "1024"}))
+    A = make_data(nb * M * K)
+    B = make_data(nb * N * K)[::-1].copy()
+    dA = torch.from_numpy(A).cuda()
+    dB = torch.from_numpy(B).cuda()
+    nnz = len(ci)
+    dP = torch.full((nb * nnz,), float("nan"), dtype=torch.float32, device="cuda")
+    plan.sddmm_batch(nb, dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
+                     stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert plan.stats()["rb_sweep"] >> 2 & 1
+    P = dP.cpu().numpy()
+    c = O.CSR.from_arrays(M, N, rp, ci)
+    for b in range(nb):
+        ref = O.sddmm_cpu(c, K, A[b * M * K:(b + 1) * M * K], B[b * N * K:(b + 1) * N * K])
+        assert np.isfinite(P[b * nnz:(b + 1) * nnz]).all()
+        assert O.check_data(ref, P[b * nnz:(b + 1) * nnz]) == 0, b
+
+
 def test_values_independent_of_layout_permutation():
     """Size-independent property: P of the same S is identical for every alpha/delta plan."""
     M, N, rp, ci = small_cases()["zipf"]
