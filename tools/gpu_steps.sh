@@ -21,6 +21,8 @@
 #                           in turn (permutation hash and clustering ms per run)
 #   ablib:<variant.so>:cfg1,cfg2[:swap]   tools/ab_lib.sh: the in-tree library against a variant
 #                           build (swap: the variant runs first in each pair)
+#   driver                  exactly the driver's BENCH command (bench.py --gpus 1 --steps 20
+#                           --warmup 5, every leg: PMC traffic, CPU baseline, vendor)
 #   driverprof              rocprofv3 --kernel-trace --stats of exactly the driver's BENCH command
 #                           (bench.py --gpus 1 --steps 20 --warmup 5; --pmc off: the in-run PMC
 #                           children would run under the tracer too) + tools/rocprof_runs.py
@@ -83,6 +85,7 @@ run_step() {
                 BSMR_DIAG=$d timeout -k 10 300 python3 tools/plan_time.py --workload reddit_like --scale "$scale" --batches 16384 > "$OUT/plan_${scale}_$d.json" 2>> "$OUT/$f.log" || return $?
                 python3 -c "import json; d=json.load(open('$OUT/plan_${scale}_$d.json')); r=list(d['runs'].values())[0]; print('scale $scale diag $d', r['row_reorder_ms'], r['rows_sha256'], r['num_clusters'], r['wall_s'])" >> "$OUT/planab_summary.txt"
             done ;;
+        driver) timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/driver.json" 2> "$OUT/driver.err" ;;
         driverprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_driver" -o run -- \
                      python3 bench.py --gpus 1 --steps 20 --warmup 5 --pmc off > "$OUT/driverprof.json" 2> "$OUT/driverprof.err" &&
                    python3 tools/rocprof_runs.py "$(ls "$OUT"/prof_driver/*/run_kernel_trace.csv "$OUT"/prof_driver/run_kernel_trace.csv 2>/dev/null | head -1)" > "$OUT/driverprof_runs.json" ;;
