@@ -419,6 +419,8 @@ struct RbArgs {
     u32 outPacked;  // 1: no out array, the metadata's low 22 bits are the CSR position
     u32 stageNt;  // 1: stage the A rows with the nt policy (Plan::stage_nt)
     u32 lateB;    // 1: phase-0 B columns / metadata loaded after the staging barrier (late_b)
+    u32 stageBlocks;  // 1 KiB LDS-DMA blocks that hold the image (RB * RBY / 1024); the rest of
+                      // the workgroup's LDS is not staged
     const u32* sortedPos;
     const uint2* itemEnt;
     // staged output by runs (RowBlockLayout::outRuns; else null): {position, slot | len << 16}, len <= 64
@@ -458,6 +460,26 @@ __device__ __forceinline__ u32 lds_chunk(u32 lr, u32 c) {
 }
 
 __device__ __forceinline__ f32x4 ld16(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// one staging LDS-DMA wave-instruction: 16 bytes per lane from g to LDS at l + 16 * lane (l
+// wave-uniform). Inline asm, so the compiler's wait-count pass does not track it: around the
+// builtin, a branch (skipping the blocks past the image) made the compiler wait (vmcnt(0)) for
+// every LDS-DMA before issuing the next. The kernels order these by their explicit
+// s_waitcnt vmcnt(0) + barrier before the image is read. AUX 2: the nt cache policy.
+// LDS byte address of a pointer into the workgroup's LDS
+__device__ __forceinline__ u32 lds_addr(const char* l) {
+    return __builtin_amdgcn_readfirstlane(static_cast<u32>(
+        reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)l)));
+}
+template <int AUX>
+__device__ __forceinline__ void rb_dma16(const char* g, const u32 m0) {
+    if constexpr (AUX == 2)
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0)
+                     : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
+                     : "memory", "m0");
+}
 
 // value of lane I of the quad in every lane of the quad
 template <int I>
@@ -740,8 +762,10 @@ __device__ __forceinline__ u32 rb_stage_rows(const RbArgs& a, const u32 q0, cons
 }
 
 // the LDS-DMAs of one row block (rows of >= 256 bytes; rowv from rb_stage_rows): every wave
-// issues exactly MAXB 1 KiB blocks, back to back (see k_sddmm_rb)
-template <int DT, int RBY, int NT, int AUX>
+// issues its 1 KiB blocks of the image back to back (see k_sddmm_rb). ALL (the pair kernel, whose
+// SGPR budget the asm form exceeds): exactly MAXB blocks per wave by the builtin, unconditionally
+// (the blocks past the image read row 0 into the unused tail)
+template <int DT, int RBY, int NT, int AUX, bool ALL>
 __device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const u32 rowv, const u32 ws,
                                                const u32 lane) {
     constexpr u32 NW = NT / 64, NCH = RBY / 16, NR = NCH >= 64 ? 1 : 64 / NCH;
@@ -758,9 +782,12 @@ __device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const 
             src = lane / NCH == k ? rk : src;
         }
         const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                         16, 0, AUX);
+        if constexpr (ALL)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                             (__attribute__((address_space(3))) void*)(As + 1024 * b),
+                                             16, 0, AUX);
+        else if (b < a.stageBlocks)
+            rb_dma16<AUX>(g, lds_addr(As) + 1024 * b);
     }
 }
 
@@ -859,6 +886,11 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
                 const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
                 src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
             }
+            // all row indices in registers before the first LDS-DMA: the compiler does not count
+            // the (inline asm) DMAs, so a wait for a later index placed between them would also
+            // wait for the DMAs issued before it (mycielskian14 K = 32: 16.3 -> 17.7 us)
+#pragma unroll
+            for (u32 i = 0; i < MAXB; ++i) asm volatile("" : "+v"(src[i]));
         }
     }
     // the loads the LDS-DMA issue waits for go first: row indices, the phase-0 piece descriptor
@@ -895,7 +927,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     auto stage = [&](auto aux_tag) {
         constexpr int AUX = decltype(aux_tag)::value;
         if constexpr (ROWV) {
-            rb_stage_issue<DT, RBY, NT, AUX>(a, As, rowv, ws, lane);
+            rb_stage_issue<DT, RBY, NT, AUX, PAIR>(a, As, rowv, ws, lane);
         } else {
             // the source chunk of lane l is the same in every block of the wave: x % NCH and
             // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
@@ -905,9 +937,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
             for (u32 i = 0; i < MAXB; ++i) {
                 const u32 b = ws + i * NW;
                 const char* g = a.A + (static_cast<size_t>(src[i]) * RBY + coff);
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                                 16, 0, AUX);
+                if (b < a.stageBlocks) rb_dma16<AUX>(g, lds_addr(As) + 1024 * b);
             }
         }
     };
@@ -1133,6 +1163,11 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             const u32 lr = 64 * (ws + i * NW) / NCH + lane / NCH, q = q0 + lr;
             src[i] = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
         }
+        // all row indices in registers before the first LDS-DMA: the compiler does not count
+        // the (inline asm) DMAs, so a wait for a later index placed between them would also
+        // wait for the DMAs issued before it (mycielskian14 K = 32: 16.3 -> 17.7 us)
+#pragma unroll
+        for (u32 i = 0; i < MAXB; ++i) asm volatile("" : "+v"(src[i]));
     }
     // the loads the LDS-DMA issue waits for go first: row indices, the phase-0 piece descriptor
     // and the first tile's metadata (one round trip together); the B columns and entry metadata
@@ -1178,18 +1213,14 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
                     src = lane / NCH == k ? rk : src;
                 }
                 const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                                 16, 0, AUX);
+                if (b < a.stageBlocks) rb_dma16<AUX>(g, lds_addr(As) + 1024 * b);
             }
         } else {
 #pragma unroll
             for (u32 i = 0; i < MAXB; ++i) {
                 const u32 b = ws + i * NW;
                 const char* g = a.A + (static_cast<size_t>(src[i]) * RBY + coff);
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                                 (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                                 16, 0, AUX);
+                if (b < a.stageBlocks) rb_dma16<AUX>(g, lds_addr(As) + 1024 * b);
             }
         }
     };
@@ -1517,6 +1548,10 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.outPacked = L.outPacked ? 1u : 0u;
     a.stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
     a.lateB = p.late_b != 0;
+    // the image's blocks only (BSMR_DIAG & 2097152, A/B only: every block of the launch's LDS, the
+    // filler past the image reading row 0 as before round 6)
+    a.stageBlocks = (p.diag & 2097152u) ? (L.NT == 1024 ? 160u : 80u)
+                                        : (L.RB * L.rowBytes + 1023) / 1024;
     a.sortedPos = L.sortedPos.data();
     a.itemEnt = L.itemEnt.data();
     a.runs = L.outRuns ? L.runs.data() : nullptr;
