@@ -1614,11 +1614,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // Sparse rows (< 64 stored entries per row) keep the small-row-block rule below (Trefethen
     // K = 512: 48-row blocks 48.1 us, 80-row blocks 51.5 us; profiles/r03v)
     const bool bigRows = item_cost_cuts && rowBytes >= 2048 && n0 >= 64ull * Rs;
-    // pipelined launch (k_sddmm_rb_pipe; Plan::pipe): two images of at most 64 KiB (128 rows of
-    // 512 B) and the result slots share the workgroup's 160 KiB
-    const bool pipeWanted = pipe == 1 && stagedWanted && rowBytes == 512;
-    const u32 ldsKb = pipeWanted ? std::min<u32>(64u, rb_lds_user ? rb_lds_kb : 64u)
-                      : (stagedWanted || bigRows) && !rb_lds_user ? stagedKb : rb_lds_kb;
+    const u32 ldsKb = (stagedWanted || bigRows) && !rb_lds_user ? stagedKb : rb_lds_kb;
     // staged 512-byte rows (C4 reddit-like x1 fp32 K = 128): 8 MiB ranges too, half the A
     // restaging for a B range twice the L2 (4.01 -> 3.89 ms over three alternating runs,
     // profiles/r03y; C3 fp16 K = 256 neutral)
@@ -1640,7 +1636,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         // smallest row block that needs no more rounds of slots, so the last round is full
         // (cop20k-like C3: 421 blocks of 288 rows = 1.6 rounds -> 505 blocks of 240 rows)
         const size_t lds0 = static_cast<size_t>(RBr) * rowBytes;
-        const u32 slots = static_cast<u32>(cus) * (lds0 > 80 * 1024 || pipeWanted ? 1u : 2u);
+        const u32 slots = static_cast<u32>(cus) * (lds0 > 80 * 1024 ? 1u : 2u);
         const u32 nRB0 = (Rs + RBr - 1) / std::max<u32>(RBr, 1);
         if (Rs && n0 < 64ull * Rs && nRB0 > slots) {
             const u32 rounds = (nRB0 + slots - 1) / slots;
@@ -1669,10 +1665,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     if (rb_rows_force > 0)  // tuning: rows per block (a multiple of 16 within the LDS budget)
         RBr = std::min(rowblock_rows(rowBytes, 160, Rs),
                        std::max<u32>(16, (static_cast<u32>(rb_rows_force) + 15) / 16 * 16));
-    if (pipeWanted) RBr = std::min<u32>(RBr, 64u * 1024u / rowBytes);
     const u32 nRB = std::max<u32>(1, (Rs + RBr - 1) / RBr);
     const size_t lds = static_cast<size_t>(RBr) * rowBytes;
-    const u32 NT = lds > 80 * 1024 || pipeWanted ? 1024 : 512;
+    const u32 NT = lds > 80 * 1024 ? 1024 : 512;
     // k_sddmm_rb takes 160 KiB (1024 threads) or 80 KiB (512) of LDS per workgroup
     const u32 wgPerCU = NT == 1024 ? 1 : 2;
     const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
@@ -1759,7 +1754,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // range sweep (sddmm.hip k_sddmm_rb_sweep): staged output over reordered rows of >= 256 bytes
     // with no kept MFMA tile; the XCD's column share in ranges of sweep_range_kb (2 MiB, or the
     // user's l2_range_kb), walked by all of the XCD's workgroups in step (BSMR_DIAG & 262144: off)
-    const bool sweepWanted = stagedWanted && !orig && !pipeWanted && hkept.empty() && rowBytes >= 256 && sweep_mode != 0 &&
+    const bool sweepWanted = stagedWanted && !orig && hkept.empty() && rowBytes >= 256 && sweep_mode != 0 &&
                              !(diag & 262144) && n > 0;
     const u32 rangeKb = sweepWanted && !l2_range_user ? sweep_range_kb : l2Kb;
     const u32 m = std::max<u32>(1, static_cast<u32>(std::ceil(
@@ -1893,8 +1888,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     std::vector<u32> nu;
     // staged output: the LDS past the A image (the launch takes 160 / 80 KiB) holds an item's
     // results when it has room for >= 1024 of them; larger items are cut to fit
-    // (pipelined: the second image and the queue words come off the tail)
-    const size_t ldsDyn = pipeWanted ? 160u * 1024u - PIPE_Q_BYTES - lds : (NT == 1024 ? 160u : 80u) * 1024u;
+    const size_t ldsDyn = (NT == 1024 ? 160u : 80u) * 1024u;
     const u32 outCap = ldsDyn > lds ? static_cast<u32>((ldsDyn - lds) / 4) : 0u;
     const bool staged = stagedWanted && outCap >= 1024;
     // chunk k of an entry range: cut where the running cost (1 per entry + piece_weight per
@@ -2325,7 +2319,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_HIP(hipGetLastError());
         BSMR_HIP(hipStreamSynchronize(s));
         L.out.release();
-        L.outLds = static_cast<u32>(pipeWanted ? 2 * lds : lds);
+        L.outLds = static_cast<u32>(lds);
         L.outCap = outCap;
         // run table (BSMR_DIAG & 8192: keep the per-result positions): up to 64 consecutive CSR
         // positions of an item's sorted slots form one run; used when no item has more runs
@@ -2391,16 +2385,6 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // the sweep kernel stores by runs only; without a run table the items (independent, in any
     // order) run on k_sddmm_rb, one workgroup each
     L.sweep = sweep && L.outRuns;
-    // pipelined: staged output by runs, no kept MFMA tile (the consumer waves run pieces only)
-    L.pipe = pipeWanted && L.outRuns && hkept.empty() && !L.sweep;
-    L.pipeImg = L.pipe ? static_cast<u32>(lds) : 0u;
-    L.pipeQ = L.pipe ? 160u * 1024u - PIPE_Q_BYTES : 0u;
-    L.pipeGrid = L.pipe ? static_cast<u32>(cus) : 0u;
-    L.pipeNext.release();
-    if (L.pipe) {
-        BSMR_CHECK(L.pipeNext.alloc(16));
-        BSMR_HIP(hipMemsetAsync(L.pipeNext.data(), 0, 16 * sizeof(u32), s));
-    }
     L.sweepW = L.sweep ? perBucket : 0;
     L.sweepSteps = L.sweep ? sweepSteps : 0;
     L.wgStart.release();

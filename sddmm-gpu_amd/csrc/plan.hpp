@@ -13,7 +13,6 @@ namespace bsmr {
 constexpr u32 TILES_PER_ITEM = 1;   // dense tiles per wave item
 constexpr u32 RES_PER_ITEM = 256;   // residual entries per panel-major wave item (panel ranges)
 constexpr u32 CM_PER_ITEM = 64;     // residual entries per column-major wave item (full launch)
-constexpr u32 PIPE_Q_BYTES = 64;   // queue hand-off words at the end of a pipelined workgroup's LDS
 constexpr u32 RB_PIECE_MAX = 16;    // entries per column-run piece (row-block layout)
 constexpr u32 XCD_BUCKETS = 8;      // MI355X XCDs: column bucket -> workgroups b with b % 8
 
@@ -121,9 +120,6 @@ struct Plan {
     // staged-output row-block layouts (rows >= 512 B) of at least this many items run in pairs
     // (k_sddmm_rb_pair; bsmr_tuning.pair_min_items)
     u32 pair_min_items = 4096;
-    // pipelined staged-output layouts of 512-byte rows (k_sddmm_rb_pipe; bsmr_tuning.pipe): 0
-    // never, 1 always
-    int pipe = 0;
     float filter_ms = 0.f;
 
     // input
@@ -216,13 +212,6 @@ struct Plan {
         // entry residual; whole-plan launches only (shards cut reordered panels)
         bool orig = false;
         DevBuf<u32> rowIds;
-        // pipelined launch (k_sddmm_rb_pipe): images at 0 and pipeImg bytes of the workgroup's
-        // LDS, the item's result slots at outLds = 2 pipeImg, the queue hand-off words at pipeQ;
-        // pipeNext: per-XCD list counters [0, 8) and the finished-workgroup count [8], reset by
-        // the last workgroup of each launch; pipeGrid: workgroups (one per CU)
-        bool pipe = false;
-        u32 pipeImg = 0, pipeQ = 0, pipeGrid = 0;
-        DevBuf<u32> pipeNext;
     };
     // rows of 128, 256, 512, 1024 and 2048 bytes, for fp32 [0, 5) and fp16/bf16 [5, 10) (tileMin)
     static constexpr int N_RB_SIZES = 5;

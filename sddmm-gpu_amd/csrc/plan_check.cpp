@@ -495,18 +495,6 @@ private:
         if (!staged && !L.outPacked && out.size() < nE) return layout_fail("output positions"), BSMR_OK;
         const u32 nRB = L.nRB, RB = L.RB;
         const u32 qbase = L.orig ? 0 : 16 * L.pa;
-        if (L.pipe) {  // k_sddmm_rb_pipe: two images, the slots and the hand-off words in 160 KiB
-            const u64 img = static_cast<u64>(RB) * L.rowBytes;
-            u64 maxEnt = 0;
-            for (u32 i = 0; i < L.nItems; ++i) maxEnt = std::max<u64>(maxEnt, itemEnt[i].y);
-            if (!staged || !L.outRuns || L.nTilesKept || L.nItems % XCD_BUCKETS || L.pipeImg < img ||
-                L.outLds < 2ull * L.pipeImg || L.outLds + 4 * maxEnt > L.pipeQ ||
-                L.pipeQ + PIPE_Q_BYTES > 160u * 1024u)
-                return layout_fail(fmt("pipelined LDS layout (image %llu B, slots at %u for %llu results, "
-                                       "hand-off at %u)", static_cast<unsigned long long>(img), L.outLds,
-                                       static_cast<unsigned long long>(maxEnt), L.pipeQ)),
-                       BSMR_OK;
-        }
         std::vector<uint8_t> hit(h_.nnz, 0), ehit(std::max<u32>(nE, 1), 0), thit(std::max<size_t>(h_.bv.size() / TILE, 1), 0);
         FirstErr fe;
         par_range(L.nItems, [&](size_t i0, size_t i1) {

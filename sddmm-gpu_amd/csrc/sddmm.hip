@@ -439,10 +439,6 @@ struct RbArgs {
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
-    // pipelined launch (RowBlockLayout::pipe, k_sddmm_rb_pipe): per-XCD list counters and the
-    // finished-workgroup count, list length per XCD, second image and hand-off words (LDS bytes)
-    u32* pipeNext;
-    u32 pipeLen, pipeImg, pipeQ;
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -685,8 +681,7 @@ template <int DT, int RBY>
 __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
                                                const Piece<RBY>& pc, const u32 sub,
                                                const u32 (&rot)[RowGeom<RBY>::NC],
-                                               const f32x4 (&bv)[RowGeom<RBY>::NC],
-                                               char* slots = nullptr) {
+                                               const f32x4 (&bv)[RowGeom<RBY>::NC]) {
     constexpr u32 G = RowGeom<RBY>::G, NC = RowGeom<RBY>::NC;
 #pragma unroll
     for (u32 k = 0; k < RowGeom<RBY>::NB; ++k) {
@@ -744,7 +739,7 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
         }
         if (sub < nb) {
             if (a.outLds)  // the slot: rank by CSR position inside the item
-                *reinterpret_cast<float*>((slots ? slots : const_cast<char*>(As) + a.outLds) +
+                *reinterpret_cast<float*>(const_cast<char*>(As) + a.outLds +
                                           4 * (pc.mm[k] & 0x3FFFFFu)) = res;
             else
                 a.P[a.outPacked ? pc.mm[k] & 0x3FFFFFu : pc.mo[k]] = res;
@@ -1357,221 +1352,6 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
         rb_item<DT, RBY, NT, 2>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
 }
 
-// ==========================================================================================
-// Pipelined row-block launch (RowBlockLayout::pipe: staged output by runs, no kept MFMA tile,
-// 512-byte rows). One persistent 1024-thread workgroup per CU takes list items of its XCD bucket
-// (blockIdx % 8, the dispatch's XCD) in order from a counter (pipeNext[bucket]); waves 0-13
-// (consumers) run the current item's pieces from one LDS image while waves 14-15 (producers)
-// stage the next item's rows into the other by LDS-DMA. The roles sit in different waves because
-// vmcnt retires in issue order per wave: a consumer's B gathers queued behind an image of
-// LDS-DMAs would wait for all of them. Per item: [consumers: pieces -> result slots | producers:
-// next image, next list index] barrier, store pass by runs (every wave), barrier; an item of the
-// image's row block is not staged again. LDS: images at 0 and pipeImg, slots at outLds = 2
-// pipeImg, hand-off words at pipeQ. Every workgroup leaves through the finished count; the last
-// one resets the counters for the next launch (launches of a plan are stream-ordered).
-// ==========================================================================================
-constexpr u32 PIPE_PW = 2;  // producer waves
-
-template <int DT, int RBY>
-__global__ __launch_bounds__(1024, 4) void k_sddmm_rb_pipe(RbArgs a) {
-    static_assert(RBY == 512, "pipelined launch: 512-byte rows (one staging row index per lane)");
-    extern __shared__ __attribute__((aligned(16))) char AsB[];
-    char* const As = AsB;
-    using Geo = RowGeom<RBY>;
-    constexpr u32 G = Geo::G, NC = Geo::NC, NW = 16, NCW = NW - PIPE_PW;
-    constexpr u32 NGC = NCW * 64 / G;             // consumer row-groups
-    constexpr u32 NCH = RBY / 16, NR = 64 / NCH;  // 16-byte chunks per row, rows per 1 KiB block
-    constexpr u32 MAXBP = 64 / NR;                // blocks per producer wave (a row index per lane)
-    static_assert(MAXBP * PIPE_PW >= 64, "the producers cover a 64 KiB image");
-    // staged output (launch_rb picks this kernel only then): no per-entry output index is loaded
-    __builtin_assume(a.outLds != 0);
-    const u32 tid = threadIdx.x, w = tid >> 6, lane = tid & 63, sub = tid % G, j = (tid & 63) / G;
-    const u32 ws = __builtin_amdgcn_readfirstlane(w);
-    const bool producer = ws >= NCW;
-    const u32 pw = producer ? ws - NCW : 0u;
-    const u32 gr = tid / G;  // consumer row-group (consumer waves: gr < NGC)
-    const u32 xq = blockIdx.x % XCD_BUCKETS;
-    u32* const qw = reinterpret_cast<u32*>(As + a.pipeQ);
-    // the bucket's next list item (one lane), NO_ITEM past the list
-    auto grab = [&]() -> u32 {
-        const u32 k = __hip_atomic_fetch_add(a.pipeNext + xq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return k < a.pipeLen ? k * XCD_BUCKETS + xq : NO_ITEM;
-    };
-    // item i (one lane or a whole wave): {row block, first piece, pieces}; row block NO_ITEM for
-    // the list's end and for padding items
-    auto info = [&](const u32 i) -> uint3 {
-        if (i == NO_ITEM) return make_uint3(NO_ITEM, 0u, 0u);
-        const uint4 it = a.items[i];
-        const u32 pend = a.itemEnd[i];
-        const bool pad = it.y == it.z && it.w == pend;
-        return make_uint3(pad ? NO_ITEM : it.x, it.w, pend - it.w);
-    };
-    // producers: row block rb's image into img (this wave's blocks pw, pw + PIPE_PW, ...); the
-    // source chunk of a lane is the same in every block of the wave (see rb_stage_issue)
-    auto stage = [&](const u32 rb, const char* img) {
-        u32 ln = lane;  // (recomputed per item, like the consumers' rotations)
-        asm volatile("" : "+v"(ln));
-        const u32 q0 = a.qbase + rb * a.RB;
-        const u32 ib = ln / NR, lr = 64 * (pw + ib * PIPE_PW) / NCH + ln % NR, q = q0 + lr;
-        u32 rowv = lr < a.RB && q < a.R ? a.rows[q] : a.row0;
-        asm volatile("" : "+v"(rowv));  // in registers before the first LDS-DMA (see k_sddmm_rb)
-        const u32 x0 = 64 * pw + ln;
-        const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
-        const u32 base = lds_addr(img);
-        // (a rolled loop: unrolled, its 64 v_readlane results were all hoisted into SGPRs)
-#pragma unroll 2
-        for (u32 i = 0; i < MAXBP; ++i) {
-            const u32 b = pw + i * PIPE_PW;
-            u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
-#pragma unroll
-            for (u32 k = 1; k < NR; ++k) {
-                const u32 rk = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR + k));
-                src = ln / NCH == k ? rk : src;
-            }
-            const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
-            if (b < a.stageBlocks) rb_dma16<0>(g, base + 1024 * b);
-        }
-    };
-    // every wave: this lane's run descriptor of item i (run w + NW lane)
-    uint2 myrun = make_uint2(0u, 0u);
-    u32 nruns = 0;
-    auto load_runs = [&](const u32 i) {
-        uint2 ir = a.itemRuns[i];
-        ir.x = __builtin_amdgcn_readfirstlane(ir.x);
-        nruns = __builtin_amdgcn_readfirstlane(ir.y);
-        const u32 jr = w + NW * lane;
-        myrun = jr < nruns ? a.runs[ir.x + jr] : make_uint2(0u, 0u);
-    };
-    // consumers: item i's pieces [p0, p0 + np) from img, results to the slots at As + a.outLds;
-    // the run descriptors are loaded in the last phase (its prefetch registers are free)
-    auto pieces = [&](const u32 i, const u32 p0, const u32 np, const char* img) {
-        char* const slots = As + a.outLds;
-        // recomputed per item, not hoisted out of the item loop, where they would hold VGPRs
-        u32 jj = j;
-        asm volatile("" : "+v"(jj));
-        u32 rot[NC];
-#pragma unroll
-        for (u32 f = 0; f < NC; ++f) rot[f] = 16u * G * ((f + jj % Geo::RR) % NC);
-        Piece<RBY> pc, pn;
-        f32x4 pre[NC], nb[NC];
-        pc.len = 0;
-        if (gr < np) load_piece<RBY>(a, p0 + gr, sub, rot, pre, pc);
-        auto fetch = [&](const u32 ph) {
-            const u32 pi = ph * NGC + ((ph & 1) ? NGC - 1 - gr : gr);
-            pn.len = 0;
-            if (pi < np) load_piece<RBY>(a, p0 + pi, sub, rot, nb, pn);
-        };
-        if (NGC < np)
-            fetch(1);
-        else
-            load_runs(i);
-        if (pc.len) residual_piece<DT, RBY>(a, img, pc, sub, rot, pre, slots);
-        for (u32 ph = 1; ph * NGC < np; ++ph) {
-            pc = pn;
-#pragma unroll
-            for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
-            if ((ph + 1) * NGC < np)
-                fetch(ph + 1);
-            else
-                load_runs(i);
-            if (pc.len) residual_piece<DT, RBY>(a, img, pc, sub, rot, pre, slots);
-        }
-    };
-    // hand-off words (qw): [0] / [1] the first two list items, [2] the item after next, [3..5]
-    // the next item's {row block, first piece, pieces}, [6..8] those of the item after it. The
-    // producers take the list index and item info of the item after next while the consumers run
-    // the current one, so neither the staging nor the consumers wait for a list round trip
-    auto put = [&](const u32 k, const uint3 v) {
-        qw[k] = v.x;
-        qw[k + 1] = v.y;
-        qw[k + 2] = v.z;
-    };
-    auto get = [&](const u32 k) {
-        return make_uint3(__builtin_amdgcn_readfirstlane(qw[k]), __builtin_amdgcn_readfirstlane(qw[k + 1]),
-                          __builtin_amdgcn_readfirstlane(qw[k + 2]));
-    };
-    if (ws == NCW && lane == 0) {
-        const u32 c = grab(), n = grab();
-        qw[0] = c;
-        qw[1] = n;
-        put(3, info(c));
-        put(6, info(n));
-    }
-    __syncthreads();
-    u32 cur = __builtin_amdgcn_readfirstlane(qw[0]), nxt = __builtin_amdgcn_readfirstlane(qw[1]);
-    uint3 ci = get(3), ni = get(6);
-    u32 imgRb = ci.x, buf = 0;
-    if (producer) {
-        if (ci.x != NO_ITEM) stage(ci.x, As);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();  // the first image landed; the hand-off words read
-    while (cur != NO_ITEM) {
-        if (producer) {
-            if (ni.x != NO_ITEM && ni.x != imgRb) stage(ni.x, As + (buf ^ 1u) * a.pipeImg);
-            if (ci.x != NO_ITEM) load_runs(cur);
-            // the item after next (after the LDS-DMAs: a load issued before them would hold the
-            // staging's first wait)
-            u32 g2 = NO_ITEM;
-            uint3 i2 = make_uint3(NO_ITEM, 0u, 0u);
-            if (ws == NCW && lane == 0 && nxt != NO_ITEM) {
-                g2 = grab();
-                i2 = info(g2);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMAs landed
-            if (ws == NCW && lane == 0) {
-                qw[2] = g2;
-                put(3, ni);
-                put(6, i2);
-            }
-        } else if (ci.x != NO_ITEM) {
-            pieces(cur, ci.y, ci.z, As + buf * a.pipeImg);
-        }
-        __syncthreads();  // slots written, next image landed, hand-off words written
-        if (ci.x != NO_ITEM) {
-            // the item's results in CSR order: wave w writes runs w, w + NW, ... (one store of up
-            // to 64 results each, four runs' LDS reads in flight together)
-            const float* res = reinterpret_cast<const float*>(As + a.outLds);
-            const u32 nr = nruns > w ? (nruns - w + NW - 1) / NW : 0u;
-            for (u32 i = 0; i < nr; i += 4) {
-                u32 pos[4], s0[4], len[4];
-                float v[4];
-#pragma unroll
-                for (u32 u = 0; u < 4; ++u) {
-                    const u32 q = min(i + u, 63u);
-                    pos[u] = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.x), q));
-                    const u32 sl = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(myrun.y), q));
-                    s0[u] = sl & 0xFFFFu;
-                    len[u] = i + u < nr ? sl >> 16 : 0u;
-                    v[u] = lane < len[u] ? res[s0[u] + lane] : 0.0f;
-                }
-#pragma unroll
-                for (u32 u = 0; u < 4; ++u)  // (runs are at most 64 long)
-                    if (lane < len[u]) a.P[pos[u] + lane] = v[u];
-            }
-        }
-        const u32 nn = __builtin_amdgcn_readfirstlane(qw[2]);
-        const uint3 n1 = get(3), n2 = get(6);
-        __syncthreads();  // no wave reads the slots, the image or the hand-off words any more
-        if (n1.x != NO_ITEM && n1.x != imgRb) {  // (the producers staged it into the other image)
-            buf ^= 1u;
-            imgRb = n1.x;
-        }
-        cur = nxt;
-        ci = n1;
-        nxt = nn;
-        ni = n2;
-    }
-    // the last workgroup out resets the counters (every list index was taken before it left)
-    if (tid == 0) {
-        const u32 done = __hip_atomic_fetch_add(a.pipeNext + XCD_BUCKETS, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-        if (done == gridDim.x - 1)
-            for (u32 k = 0; k <= XCD_BUCKETS; ++k)
-                __hip_atomic_exchange(a.pipeNext + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 // the longest a workgroup waits for its XCD's slowest workgroup to leave a step (s_memrealtime
 // ticks, 100 MHz): the wait only keeps the XCD's workgroups inside a window of column ranges (B
 // lines shared in L2); past it the workgroup goes on, so no step ever depends on co-residency
@@ -1787,18 +1567,6 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     // the range sweep's per-XCD step counters serve one launch of one batch: batched launches run
     // a sweep layout's items as independent workgroups on k_sddmm_rb (items are self-contained)
     const bool sweep = L.sweep && nb == 1;
-    // pipelined (one persistent workgroup per CU, RowBlockLayout::pipe): whole-plan launches of
-    // one batch, not under the profiling ablations; otherwise the layout's items run on
-    // k_sddmm_rb (its slots sit past both images, within the LDS the launch takes)
-    const bool pipe = L.pipe && nb == 1 && mode == 3 && L.rowBytes == 512 &&
-                      L.nItems % XCD_BUCKETS == 0 && !(p.diag & (8u | 32u | 64u | 128u));
-    if (pipe) {
-        a.pairs = 0;
-        a.pipeNext = L.pipeNext.data();
-        a.pipeLen = L.nItems / XCD_BUCKETS;
-        a.pipeImg = L.pipeImg;
-        a.pipeQ = L.pipeQ;
-    }
     if (sweep) {
         a.pairs = 0;
         a.wgStart = L.wgStart.data();
@@ -1831,14 +1599,14 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
      : L.rowBytes == 1024 ? BSMR_RB(DT, 1024)                                             \
                           : BSMR_RB(DT, 2048))
     switch (dtype) {
-        case BSMR_F32: fn = pipe ? k_sddmm_rb_pipe<0, 512> : BSMR_RB2(0); break;
-        case BSMR_F16: fn = pipe ? k_sddmm_rb_pipe<1, 512> : BSMR_RB2(1); break;
-        default: fn = pipe ? k_sddmm_rb_pipe<2, 512> : BSMR_RB2(2); break;
+        case BSMR_F32: fn = BSMR_RB2(0); break;
+        case BSMR_F16: fn = BSMR_RB2(1); break;
+        default: fn = BSMR_RB2(2); break;
     }
 #undef BSMR_RB2
 #undef BSMR_RB
     // k_sddmm_rb stages a fixed 160 / 80 KiB per workgroup (the image and an unused tail)
-    const u32 grid = pipe ? L.pipeGrid : sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
+    const u32 grid = sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
     hipLaunchKernelGGL(fn, dim3(grid, nb), dim3(L.NT),
                        (L.NT == 1024 ? 160 : 80) * 1024, s, a);
     BSMR_HIP(hipGetLastError());
@@ -1877,7 +1645,7 @@ int launch_panels(SddmmArgs a, hipStream_t s) {
 // in L2, no stores) nor nt staging / early B loads
 bool rb_uses_pairs(const Plan& p, const Plan::RowBlockLayout& L) {
     const bool stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
-    return !L.sweep && !L.pipe && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= p.pair_min_items &&
+    return !L.sweep && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= p.pair_min_items &&
            L.nTilesKept == 0 && L.nItems % (2 * XCD_BUCKETS) == 0 && !stageNt && p.late_b != 0 &&
            !(p.diag & (8u | 32u | 64u | 128u | 16384u));
 }
