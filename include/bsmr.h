@@ -22,14 +22,15 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 10 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 11 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
                               the plan options (no environment reads in the library);
                               7: bsmr_tuning.out_packed; 8: bsmr_tuning.sweep*, rb_sweep;
                               9: bsmr_tuning.cluster_filter, filter stats;
                               10: bsmr_plan_check, bsmr_check_rphm_arrays, BSMR_ERR_CHECK,
-                              bsmr_tuning.pair_min_items, stats rb_pairs */
+                              bsmr_tuning.pair_min_items, stats rb_pairs;
+                              11: bsmr_tuning.batches, stats rb_batches */
 
 typedef enum {
     BSMR_OK = 0,
@@ -149,6 +150,10 @@ typedef struct {
                                   with at least this many list items run two items per workgroup
                                   (k_sddmm_rb_pair, the second item's staging under the first's
                                   stores); -1 = 4096 */
+    int32_t batches;           /* BSMR_BATCHES: row-block launches of rows <= 512 B deal column-run
+                                  pieces to waves in batches from an LDS counter instead of fixed
+                                  phases; 0 never, 1 always, -1 = auto (512-byte rows, items of
+                                  >= 2 pieces per row-group) */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -251,6 +256,8 @@ typedef struct {
     float cluster_filter_ms;
     /* bit i set: row-block layout i (as rb_rows) launches two items per workgroup (pairs) */
     uint32_t rb_pairs;
+    /* bit i set: row-block layout i (as rb_rows) deals its pieces in dynamic batches */
+    uint32_t rb_batches;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

@@ -49,7 +49,8 @@ class Tuning(C.Structure):
                 ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
                 ("item_sched", C.c_int32), ("out_packed", C.c_int32), ("sweep", C.c_int32),
                 ("sweep_range_kb", C.c_int32), ("sweep_split", C.c_float), ("sweep_slack", C.c_int32),
-                ("cluster_filter", C.c_int32), ("pair_min_items", C.c_int32)]
+                ("cluster_filter", C.c_int32), ("pair_min_items", C.c_int32),
+                ("batches", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -82,7 +83,8 @@ class PlanStats(C.Structure):
                 ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5),
                 ("dense_sampled_tiles", C.c_uint32), ("rb_orig_rows", C.c_uint32),
                 ("rb_sweep", C.c_uint32), ("cluster_filter_used", C.c_uint32),
-                ("cluster_filter_ms", C.c_float), ("rb_pairs", C.c_uint32)]
+                ("cluster_filter_ms", C.c_float), ("rb_pairs", C.c_uint32),
+                ("rb_batches", C.c_uint32)]
 
     def as_dict(self):
         d = {}
@@ -122,7 +124,7 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 10  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 11  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [

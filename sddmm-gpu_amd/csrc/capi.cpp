@@ -40,6 +40,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->sweep_split = -1.0f;
     t->cluster_filter = -1;
     t->pair_min_items = -1;
+    t->batches = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -93,6 +94,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     geti("BSMR_SWEEP_SLACK", t->sweep_slack);
     get3("BSMR_CLUSTER_FILTER", t->cluster_filter);
     geti("BSMR_PAIR_MIN_ITEMS", t->pair_min_items);
+    get3("BSMR_BATCHES", t->batches);
     return n;
 }
 
@@ -153,6 +155,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->sweep_slack >= 0) p.sweep_slack = static_cast<u32>(t->sweep_slack);
         if (t->cluster_filter >= 0) p.cluster_filter = t->cluster_filter ? 1 : 0;
         if (t->pair_min_items >= 0) p.pair_min_items = static_cast<u32>(t->pair_min_items);
+        if (t->batches >= 0) p.batches = t->batches ? 1 : 0;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -372,6 +375,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         if (L.rowBytes && L.orig) s->rb_orig_rows |= 1u << i;
         if (L.rowBytes && L.sweep) s->rb_sweep |= 1u << i;
         if (L.rowBytes && rb_uses_pairs(p, L)) s->rb_pairs |= 1u << i;
+        if (L.rowBytes && L.dynBatches) s->rb_batches |= 1u << i;
     }
     s->dense_sampled_tiles = p.dense.built ? p.dense.nonempty : 0;
     return BSMR_OK;

@@ -1470,7 +1470,12 @@ u32 kept_warp_mask(u32 B) {
 // Rows per row block for rows of rowBytes: a multiple of 16 with RB * rowBytes within the LDS
 // budget, at most 1024 (10-bit local row in the entry metadata) and no more than the matrix needs.
 u32 rowblock_rows(u32 rowBytes, u32 lds_kb, u32 R) {
-    u32 rb = static_cast<u32>(static_cast<u64>(lds_kb) * 1024 / rowBytes / 16 * 16);
+    // (rows of <= 512 B: the workgroup's last LDS word is the piece-batch counter of k_sddmm_rb /
+    // k_sddmm_rb_pair, so a whole-LDS budget leaves it out; an 80 KiB image is caught where the
+    // block size is final)
+    u64 bytes = static_cast<u64>(lds_kb) * 1024;
+    if (rowBytes <= 512 && bytes >= 160u * 1024u) bytes = 160u * 1024u - 16u;
+    u32 rb = static_cast<u32>(bytes / rowBytes / 16 * 16);
     rb = std::min<u32>(std::max<u32>(rb, 16), 1024);
     return std::min<u32>(rb, std::max<u32>((R + 15) / 16 * 16, 16));
 }
@@ -1665,6 +1670,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     if (rb_rows_force > 0)  // tuning: rows per block (a multiple of 16 within the LDS budget)
         RBr = std::min(rowblock_rows(rowBytes, 160, Rs),
                        std::max<u32>(16, (static_cast<u32>(rb_rows_force) + 15) / 16 * 16));
+    // rows of <= 512 B: an image of exactly 80 KiB would fill a 512-thread workgroup's LDS, whose
+    // last word is the piece-batch counter (160 KiB images are excluded by rowblock_rows)
+    if (rowBytes <= 512 && static_cast<size_t>(RBr) * rowBytes == 80u * 1024u && RBr > 16) RBr -= 16;
     const u32 nRB = std::max<u32>(1, (Rs + RBr - 1) / RBr);
     const size_t lds = static_cast<size_t>(RBr) * rowBytes;
     const u32 NT = lds > 80 * 1024 ? 1024 : 512;
@@ -1889,7 +1897,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // staged output: the LDS past the A image (the launch takes 160 / 80 KiB) holds an item's
     // results when it has room for >= 1024 of them; larger items are cut to fit
     const size_t ldsDyn = (NT == 1024 ? 160u : 80u) * 1024u;
-    const u32 outCap = ldsDyn > lds ? static_cast<u32>((ldsDyn - lds) / 4) : 0u;
+    // (the last 16 bytes: the piece-batch counter)
+    const u32 outCap = ldsDyn > lds + 16 ? static_cast<u32>((ldsDyn - lds - 16) / 4) : 0u;
     const bool staged = stagedWanted && outCap >= 1024;
     // chunk k of an entry range: cut where the running cost (1 per entry + piece_weight per
     // column-run piece start) crosses k / nch of the range's cost, so chunks of single-entry
@@ -2385,6 +2394,19 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // the sweep kernel stores by runs only; without a run table the items (independent, in any
     // order) run on k_sddmm_rb, one workgroup each
     L.sweep = sweep && L.outRuns;
+    // dynamic piece batches (Plan::batches; kernels for rows of <= 512 B): after its first batch
+    // of 64 / G pieces a wave takes the next from an LDS counter, which balances the waves of
+    // items with several pieces per row-group. Measured (profiles/r05bt, forced on against off):
+    // 512-byte rows with 2.4 / 6.5 / 6.8 pieces per row-group (mycielskian14 K = 128, C3, C4
+    // x0.5) -4.5 / -2.4 / -2.2 %, C2's 1.4 +5 %; 128- and 256-byte rows (mycielskian15 K = 32,
+    // Trefethen K = 64: little work per entry behind each counter round trip) +2 to +8 %. Auto:
+    // 512-byte rows from batch_min_phases pieces per row-group
+    {
+        const u32 NGl = NT / 4;  // row-groups (G = 4 for rows of <= 512 B)
+        const double perItem = L.nWorkItems ? static_cast<double>(pieces.size()) / L.nWorkItems : 0.0;
+        L.dynBatches = rowBytes <= 512 && !L.sweep &&
+                       (batches == 1 || (batches < 0 && rowBytes == 512 && perItem >= batch_min_phases * NGl));
+    }
     L.sweepW = L.sweep ? perBucket : 0;
     L.sweepSteps = L.sweep ? sweepSteps : 0;
     L.wgStart.release();

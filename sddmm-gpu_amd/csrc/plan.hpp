@@ -120,6 +120,11 @@ struct Plan {
     // staged-output row-block layouts (rows >= 512 B) of at least this many items run in pairs
     // (k_sddmm_rb_pair; bsmr_tuning.pair_min_items)
     u32 pair_min_items = 4096;
+    // dynamic piece batches of the row-block launch (rows of <= 512 B; bsmr_tuning.batches): 1
+    // always, 0 never, -1 for 512-byte rows whose items hold >= batch_min_phases pieces per
+    // row-group on average
+    int batches = -1;
+    double batch_min_phases = 2.0;
     float filter_ms = 0.f;
 
     // input
@@ -212,6 +217,8 @@ struct Plan {
         // entry residual; whole-plan launches only (shards cut reordered panels)
         bool orig = false;
         DevBuf<u32> rowIds;
+        // dynamic piece batches (k_sddmm_rb / k_sddmm_rb_pair<.., true>; Plan::batches)
+        bool dynBatches = false;
     };
     // rows of 128, 256, 512, 1024 and 2048 bytes, for fp32 [0, 5) and fp16/bf16 [5, 10) (tileMin)
     static constexpr int N_RB_SIZES = 5;

@@ -495,6 +495,23 @@ private:
         if (!staged && !L.outPacked && out.size() < nE) return layout_fail("output positions"), BSMR_OK;
         const u32 nRB = L.nRB, RB = L.RB;
         const u32 qbase = L.orig ? 0 : 16 * L.pa;
+        {
+            // the workgroup's LDS (launch_rb: 160 KiB at 1024 threads, 80 KiB at 512) holds the
+            // image and, for staged output, the largest item's result slots past it; rows of
+            // <= 512 B keep the last 16 bytes for the piece-batch counter
+            const u64 dyn = (L.NT == 1024 ? 160u : 80u) * 1024u, img = static_cast<u64>(RB) * L.rowBytes;
+            u64 maxEnt = 0;
+            if (staged)
+                for (u32 i = 0; i < L.nItems; ++i) maxEnt = std::max<u64>(maxEnt, itemEnt[i].y);
+            const u64 used = (staged ? std::max<u64>(L.outLds, img) + 4 * maxEnt : img) +
+                             (L.rowBytes <= 512 ? 16u : 0u);
+            if (used > dyn || (staged && L.outLds < img))
+                return layout_fail(fmt("LDS layout: image %llu B, %llu result slots at %u, %llu B per workgroup",
+                                       static_cast<unsigned long long>(img),
+                                       static_cast<unsigned long long>(maxEnt), L.outLds,
+                                       static_cast<unsigned long long>(dyn))),
+                       BSMR_OK;
+        }
         std::vector<uint8_t> hit(h_.nnz, 0), ehit(std::max<u32>(nE, 1), 0), thit(std::max<size_t>(h_.bv.size() / TILE, 1), 0);
         FirstErr fe;
         par_range(L.nItems, [&](size_t i0, size_t i1) {

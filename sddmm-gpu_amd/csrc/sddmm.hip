@@ -747,6 +747,51 @@ __device__ __forceinline__ void residual_piece(const RbArgs& a, const char* As,
     }
 }
 
+// Dynamic piece batches (RowBlockLayout::dynBatches, rows of <= 512 B): batch b = the item's
+// pieces [b GW, (b + 1) GW), GW = 64 / G, one per row-group of a wave. Wave w runs batch w first
+// (the static phase 0), then takes the next batch from a counter in the workgroup's last LDS word
+// (the layout keeps it free), so waves whose pieces were short or whose gathers were fast take
+// more of an item with many pieces per row-group. The next batch's piece is loaded while the
+// current one computes, as in the static phases. Returns after the wave's last batch.
+constexpr u32 BATCH_CTR_BYTES = 16;  // the counter's share of the workgroup's LDS (its end)
+template <int DT, int RBY, int NT, typename LoadRuns>
+__device__ __forceinline__ void rb_batches(const RbArgs& a, const char* As, const u32 p0, const u32 np,
+                                           const u32 gr, const u32 sub, const u32 (&rot)[RowGeom<RBY>::NC],
+                                           Piece<RBY>& pc, f32x4 (&pre)[RowGeom<RBY>::NC], LoadRuns&& load_runs) {
+    constexpr u32 NC = RowGeom<RBY>::NC, GW = 64 / RowGeom<RBY>::G, NW = NT / 64;
+    u32* const ctr = reinterpret_cast<u32*>(const_cast<char*>(As) + (NT == 1024 ? 160u : 80u) * 1024u - 4u);
+    auto grab = [&]() -> u32 {
+        u32 v = 0;
+        if ((threadIdx.x & 63) == 0)
+            v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return NW + static_cast<u32>(__builtin_amdgcn_readfirstlane(static_cast<int>(v)));
+    };
+    Piece<RBY> pn;
+    f32x4 nb[NC];
+    auto fetch = [&](const u32 b) {
+        const u32 pi = b * GW + gr % GW;
+        pn.len = 0;
+        if (pi < np) load_piece<RBY>(a, p0 + pi, sub, rot, nb, pn);
+    };
+    u32 bn = grab();
+    if (bn * GW < np)
+        fetch(bn);
+    else
+        load_runs();
+    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+    while (bn * GW < np) {
+        pc = pn;
+#pragma unroll
+        for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
+        bn = grab();
+        if (bn * GW < np)
+            fetch(bn);
+        else
+            load_runs();
+        if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+    }
+}
+
 constexpr u32 NO_ITEM = 0xFFFFFFFFu;
 // run values a wave holds in registers while the next item's staging is issued (pairs)
 constexpr u32 PAIR_RUNS_PER_WAVE = 16;
@@ -797,7 +842,7 @@ __device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const 
 // slots have been read into registers, so the next image lands while this item's stores drain.
 // Returns whether next's staging was issued (false: next is padding, or this item holds more
 // runs per wave than PAIR_RUNS_PER_WAVE and stored them the plain way).
-template <int DT, int RBY, int NT, int OM>
+template <int DT, int RBY, int NT, int OM, bool DYN = false>
 __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx, const bool prestaged,
                                         const u32 next) {
     // OM (output mode): 0 = one store per entry (a.outLds == 0), 1 = staged output (slots in
@@ -959,6 +1004,10 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // not left to the compiler's wait insertion at the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (DYN) {  // (after the barrier: the pair kernel's filler blocks cover the last word)
+        if (tid == 0) *reinterpret_cast<u32*>(As + (NT == 1024 ? 160u : 80u) * 1024u - 4u) = 0u;
+        __syncthreads();
+    }
     if (LEAN || a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
         if constexpr (!LEAN)
@@ -977,21 +1026,25 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
     // alternates long and short pieces; phase ph's piece and B column are loaded while phase
     // ph - 1 computes (two register sets)
-    Piece<RBY> pn;
-    f32x4 nb[NC];
-    auto fetch = [&](const u32 ph) {
-        const u32 pi = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
-        pn.len = 0;
-        if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
-    };
-    if (NG < np) fetch(1);
-    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
-    for (u32 ph = 1; ph * NG < np; ++ph) {
-        pc = pn;
-#pragma unroll
-        for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
-        if ((ph + 1) * NG < np) fetch(ph + 1);
+    if constexpr (DYN) {
+        rb_batches<DT, RBY, NT>(a, As, it.w, np, gr, sub, rot, pc, pre, [] {});
+    } else {
+        Piece<RBY> pn;
+        f32x4 nb[NC];
+        auto fetch = [&](const u32 ph) {
+            const u32 pi = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
+            pn.len = 0;
+            if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
+        };
+        if (NG < np) fetch(1);
         if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+        for (u32 ph = 1; ph * NG < np; ++ph) {
+            pc = pn;
+#pragma unroll
+            for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
+            if ((ph + 1) * NG < np) fetch(ph + 1);
+            if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+        }
     }
     // (behind the pieces, not in their last phase: live across the phase loop, the descriptors
     // cost the loop VGPRs; a wave that ends early has them back before the store-pass barrier)
@@ -1095,7 +1148,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
 // (This single-item kernel keeps its own body rather than calling rb_item: the shared form
 // measured 3 % slower on C2, 10.70 vs 10.46 us on one box, with the same instruction count; the
 // pair kernel below uses rb_item.)
-template <int DT, int RBY, int NT>
+template <int DT, int RBY, int NT, bool DYN>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char AsB[];
     char* As = AsB;
@@ -1238,6 +1291,8 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // every LDS-DMA of the workgroup has landed before any wave reads the image or writes the
     // staged-output slots (the blocks past the image land in the tail those slots use); explicit,
     // not left to the compiler's wait insertion at the barrier
+    if constexpr (DYN)  // (the image-only staging never writes the last word)
+        if (tid == 0) *reinterpret_cast<u32*>(As + (NT == 1024 ? 160u : 80u) * 1024u - 4u) = 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (a.lateB) {
@@ -1256,27 +1311,31 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
     // alternates long and short pieces; phase ph's piece and B column are loaded while phase
     // ph - 1 computes (two register sets)
-    Piece<RBY> pn;
-    f32x4 nb[NC];
-    auto fetch = [&](const u32 ph) {
-        const u32 pi = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
-        pn.len = 0;
-        if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
-    };
-    if (NG < np)
-        fetch(1);
-    else
-        load_runs();
-    if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
-    for (u32 ph = 1; ph * NG < np; ++ph) {
-        pc = pn;
-#pragma unroll
-        for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
-        if ((ph + 1) * NG < np)
-            fetch(ph + 1);
+    if constexpr (DYN) {
+        rb_batches<DT, RBY, NT>(a, As, it.w, np, gr, sub, rot, pc, pre, load_runs);
+    } else {
+        Piece<RBY> pn;
+        f32x4 nb[NC];
+        auto fetch = [&](const u32 ph) {
+            const u32 pi = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
+            pn.len = 0;
+            if (pi < np) load_piece<RBY>(a, it.w + pi, sub, rot, nb, pn);
+        };
+        if (NG < np)
+            fetch(1);
         else
             load_runs();
         if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+        for (u32 ph = 1; ph * NG < np; ++ph) {
+            pc = pn;
+#pragma unroll
+            for (u32 f = 0; f < NC; ++f) pre[f] = nb[f];
+            if ((ph + 1) * NG < np)
+                fetch(ph + 1);
+            else
+                load_runs();
+            if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
+        }
     }
     for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
         dt.load(a, a.tileIds[t], q0, tb);
@@ -1338,7 +1397,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
 // Pairs (staged output by runs): a workgroup runs list positions 2j and 2j + 1 of its XCD
 // (items are laid out [position * 8 + x]; workgroup g runs on XCD g % 8), the second item's
 // staging issued in the first one's store pass (rb_item)
-template <int DT, int RBY, int NT>
+template <int DT, int RBY, int NT, bool DYN>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char AsB[];
     char* As = AsB;
@@ -1348,8 +1407,8 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
         a.P += blockIdx.y * a.bP;
     }
     const u32 x = blockIdx.x % XCD_BUCKETS, i0 = (blockIdx.x / XCD_BUCKETS) * 2 * XCD_BUCKETS + x;
-    if (rb_item<DT, RBY, NT, 2>(a, As, i0, false, i0 + XCD_BUCKETS))
-        rb_item<DT, RBY, NT, 2>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
+    if (rb_item<DT, RBY, NT, 2, DYN>(a, As, i0, false, i0 + XCD_BUCKETS))
+        rb_item<DT, RBY, NT, 2, DYN>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
 }
 
 // the longest a workgroup waits for its XCD's slowest workgroup to leave a step (s_memrealtime
@@ -1410,12 +1469,19 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_sweep(RbArgs a) {
 }
 
 template <int DT, int RBY>
-void (*pick_rb(const u32 NT, const bool pairs, const bool sweep))(RbArgs) {
+void (*pick_rb(const u32 NT, const bool pairs, const bool sweep, const bool dyn))(RbArgs) {
+    // (dynamic batches: rows of <= 512 B, RowBlockLayout::dynBatches)
     if constexpr (RBY >= 256) {  // (launch_rb enables pairs from 512-byte rows)
         if (sweep && NT == 1024) return k_sddmm_rb_sweep<DT, RBY, 1024>;
-        if (pairs) return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024> : k_sddmm_rb_pair<DT, RBY, 512>;
+        if (pairs) {
+            if constexpr (RBY <= 512)
+                if (dyn) return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024, true> : k_sddmm_rb_pair<DT, RBY, 512, true>;
+            return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024, false> : k_sddmm_rb_pair<DT, RBY, 512, false>;
+        }
     }
-    return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024> : k_sddmm_rb<DT, RBY, 512>;
+    if constexpr (RBY <= 512)
+        if (dyn) return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true> : k_sddmm_rb<DT, RBY, 512, true>;
+    return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false> : k_sddmm_rb<DT, RBY, 512, false>;
 }
 
 static_assert(TILES_PER_ITEM == 1, "dense work items are single tiles (tile id = item id)");
@@ -1591,7 +1657,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, sweep)
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, sweep, L.dynBatches && !sweep)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \

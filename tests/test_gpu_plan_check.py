@@ -83,6 +83,18 @@ LAYOUTS = {
     "colmajor": (ZIPF, 128, F32, {"layout": "colmajor"}),
     "colmajor_half": (ZIPF, 128, F16, {"layout": "colmajor"}),
     "dense_sampled": (lambda: synth.uniform_mask(512, 0.1, 7), 512, BF16, {}),
+    # dynamic piece batches (rows of <= 512 B; waves take batches from an LDS counter): forced on
+    # packed / staged / paired / half / 128- and 256-byte-row / original-order layouts, and on a
+    # pattern of many single-entry pieces per item (several batches per wave)
+    "batches_packed": (ZIPF, 128, F32, {"tuning": {"batches": 1}}),
+    "batches_k32": (ZIPF, 32, F32, {"tuning": {"batches": 1}}),
+    "batches_k64": (ZIPF, 64, F32, {"tuning": {"batches": 1}}),
+    "batches_staged": (WIDE, 128, F32, {"tuning": {"out_staged": 1, "batches": 1}}),
+    "batches_pairs": (WIDE, 128, F32, {"tuning": {"out_staged": 1, "pair_min_items": 16, "batches": 1}}),
+    "batches_half": (WIDE, 256, F16, {"tuning": {"out_staged": 1, "tile_min_half": 257, "batches": 1}}),
+    "batches_orig": (lambda: synth.trefethen(3000), 64, F32, {"tuning": {"orig_rows": 1, "batches": 1}}),
+    "batches_scattered": (lambda: synth.random_rows(4000, 60000, 40, seed=12, zipf=0.6), 128, F32,
+                          {"tuning": {"batches": 1}}),
 }
 
 
@@ -106,6 +118,10 @@ def test_plan_and_launch_layout_pass(name, capfd):
         assert st["rb_orig_rows"] != 0
     if name == "kept_tiles_f32":
         assert max(st["rb_tiles"]) > 0
+    if name.startswith("batches"):
+        assert st["rb_batches"] != 0, st
+    if name == "batches_pairs":
+        assert st["rb_pairs"] & (1 << 2), st
 
 
 def test_pairs_with_padding_inside_a_pair():
