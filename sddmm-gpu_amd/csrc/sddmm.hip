@@ -1955,6 +1955,27 @@ extern "C" int bsmr_debug_rb_items(const bsmr_plan* plan, uint32_t K, int dtype,
     return BSMR_OK;
 }
 
+// debug: the whole plan's row-block layout for (K, dtype) as {items (4 u32 each: row block, tile
+// begin, tile end, piece begin), item ends, pieces (2 u32 each)}: *len = 4 n + n + 2 p + 2 with
+// host_out[0] = n items, [1] = p pieces (tools/phase_balance.py; not in the header)
+extern "C" int bsmr_debug_rb_pieces(const bsmr_plan* plan, uint32_t K, int dtype, uint32_t* host_out,
+                                    uint64_t* len) {
+    if (!plan) return BSMR_ERR_INVALID;
+    const Plan& p = plan->p;
+    const Plan::RowBlockLayout* L = nullptr;
+    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
+    const u64 n = L ? L->nItems : 0, np = L ? L->nPieces : 0;
+    if (len) *len = 2 + 5 * n + 2 * np;
+    if (host_out && L) {
+        host_out[0] = static_cast<uint32_t>(n);
+        host_out[1] = static_cast<uint32_t>(np);
+        BSMR_HIP(hipMemcpy(host_out + 2, L->items.data(), n * sizeof(uint4), hipMemcpyDeviceToHost));
+        BSMR_HIP(hipMemcpy(host_out + 2 + 4 * n, L->itemEnd.data(), n * sizeof(u32), hipMemcpyDeviceToHost));
+        BSMR_HIP(hipMemcpy(host_out + 2 + 5 * n, L->pieces.data(), np * sizeof(uint2), hipMemcpyDeviceToHost));
+    }
+    return BSMR_OK;
+}
+
 // debug timeline of the last traced launch (BSMR_DIAG & 32): 4 u64 per wave (not in the header)
 extern "C" int bsmr_debug_trace(const bsmr_plan* plan, uint64_t* host_out, uint64_t* len) {
     if (!plan) return BSMR_ERR_INVALID;
