@@ -807,17 +807,21 @@ __device__ __forceinline__ u32 rb_stage_rows(const RbArgs& a, const u32 q0, cons
 }
 
 // the LDS-DMAs of one row block (rows of >= 256 bytes; rowv from rb_stage_rows): every wave
-// issues its 1 KiB blocks of the image back to back (see k_sddmm_rb). ALL (the pair kernel, whose
-// SGPR budget the asm form exceeds): exactly MAXB blocks per wave by the builtin, unconditionally
-// (the blocks past the image read row 0 into the unused tail)
-template <int DT, int RBY, int NT, int AUX, bool ALL>
-__device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const u32 rowv, const u32 ws,
+// issues its 1 KiB blocks of the image back to back (see k_sddmm_rb)
+template <int DT, int RBY, int NT, int AUX>
+__device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, u32 rowv, const u32 ws,
                                                const u32 lane) {
     constexpr u32 NW = NT / 64, NCH = RBY / 16, NR = NCH >= 64 ? 1 : 64 / NCH;
+    // the row indices in registers before the first LDS-DMA: the compiler does not count the
+    // (inline asm) DMAs, so a wait for the indices inside the rolled loop (at its head) would also
+    // wait for every DMA issued before it
+    asm volatile("" : "+v"(rowv));
     constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
     const u32 x0 = 64 * ws + lane;
     const u32 coff = 16 * lds_chunk<DT>(x0 / NCH, x0 % NCH);
-#pragma unroll
+    // (a loop rolled by two: fully unrolled, its v_readlane results were all hoisted into SGPRs,
+    // which the pair kernel's two items cannot spare)
+#pragma unroll 2
     for (u32 i = 0; i < MAXB; ++i) {
         const u32 b = ws + i * NW;
         u32 src = static_cast<u32>(__builtin_amdgcn_readlane(static_cast<int>(rowv), i * NR));
@@ -827,12 +831,7 @@ __device__ __forceinline__ void rb_stage_issue(const RbArgs& a, char* As, const 
             src = lane / NCH == k ? rk : src;
         }
         const char* g = a.A + (static_cast<size_t>(src) * RBY + coff);
-        if constexpr (ALL)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                             (__attribute__((address_space(3))) void*)(As + 1024 * b),
-                                             16, 0, AUX);
-        else if (b < a.stageBlocks)
-            rb_dma16<AUX>(g, lds_addr(As) + 1024 * b);
+        if (b < a.stageBlocks) rb_dma16<AUX>(g, lds_addr(As) + 1024 * b);
     }
 }
 
@@ -972,7 +971,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     auto stage = [&](auto aux_tag) {
         constexpr int AUX = decltype(aux_tag)::value;
         if constexpr (ROWV) {
-            rb_stage_issue<DT, RBY, NT, AUX, PAIR>(a, As, rowv, ws, lane);
+            rb_stage_issue<DT, RBY, NT, AUX>(a, As, rowv, ws, lane);
         } else {
             // the source chunk of lane l is the same in every block of the wave: x % NCH and
             // (x / NCH) & 3 for x = 64 (ws + i NW) + l do not depend on i (NW = 16 or 8, NCH >= 8)
@@ -1002,12 +1001,12 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // every LDS-DMA of the workgroup has landed before any wave reads the image or writes the
     // staged-output slots (the blocks past the image land in the tail those slots use); explicit,
     // not left to the compiler's wait insertion at the barrier
+    // the batch counter (no LDS-DMA writes the last word; every grab of the pair's previous item
+    // ended before its store-pass barrier)
+    if constexpr (DYN)
+        if (tid == 0) *reinterpret_cast<u32*>(As + (NT == 1024 ? 160u : 80u) * 1024u - 4u) = 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if constexpr (DYN) {  // (after the barrier: the pair kernel's filler blocks cover the last word)
-        if (tid == 0) *reinterpret_cast<u32*>(As + (NT == 1024 ? 160u : 80u) * 1024u - 4u) = 0u;
-        __syncthreads();
-    }
     if (LEAN || a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
         if constexpr (!LEAN)
@@ -1063,7 +1062,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
         const u32 nr = irun.y > w ? (irun.y - w + NW - 1) / NW : 0u;
         if constexpr (PAIR && ROWV) {
             // pairs: this wave's run values into registers, a barrier (no wave reads a slot
-            // any more), the next item's LDS-DMAs (their filler blocks overwrite the slots),
+            // any more; the next image may reach into the slots), the next item's LDS-DMAs,
             // then this item's stores, all in flight together
             if (has_next && __builtin_amdgcn_readfirstlane(irun.y) <= NW * PAIR_RUNS_PER_WAVE) {
                 float v[PAIR_RUNS_PER_WAVE];
@@ -1614,9 +1613,10 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.outPacked = L.outPacked ? 1u : 0u;
     a.stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
     a.lateB = p.late_b != 0;
-    // the image's blocks only (BSMR_DIAG & 2097152, A/B only: every block of the launch's LDS, the
-    // filler past the image reading row 0 as before round 6)
-    a.stageBlocks = (p.diag & 2097152u) ? (L.NT == 1024 ? 160u : 80u)
+    // the image's blocks only (BSMR_DIAG & 2097152, A/B only: every block of the launch's LDS but
+    // the last, which holds the piece-batch counter — the filler past the image reading row 0, as
+    // before round 5)
+    a.stageBlocks = (p.diag & 2097152u) ? (L.NT == 1024 ? 159u : 79u)
                                         : (L.RB * L.rowBytes + 1023) / 1024;
     a.sortedPos = L.sortedPos.data();
     a.itemEnt = L.itemEnt.data();
