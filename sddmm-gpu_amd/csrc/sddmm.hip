@@ -902,12 +902,11 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     // lr = x / NCH at physical chunk pc = x % NCH, read from the logical chunk lds_chunk(lr, pc)
     // of A[rows[q0 + lr]] (the XOR is an involution). The row indices of the wave's blocks are
     // loaded once, one per lane, and handed to the block's lanes with v_readlane + select.
-    // Every wave stages exactly MAXB blocks b = w + i NW (the launch's whole LDS: 160 KiB at 1024
-    // threads, 80 KiB at 512), unconditionally: blocks past the image land in its unused tail
-    // (their rows read A row 0). A branch around a block, or any LDS instruction between two
-    // LDS-DMAs (a ds_bpermute hand-out of the row indices did this), makes the compiler wait
-    // (vmcnt(0)) for each LDS-DMA before issuing the next, which serialised the staging
-    // (C2: 12.8 -> 12.0 us once removed).
+    // Wave w stages the image's blocks b = w + i NW < stageBlocks, back to back, by inline-asm
+    // LDS-DMAs (rb_dma16): around the builtin, a branch (skipping a block) or any LDS instruction
+    // between two LDS-DMAs made the compiler wait (vmcnt(0)) for each LDS-DMA before issuing the
+    // next, which serialised the staging (C2: 12.8 -> 12.0 us once removed); until round 5 every
+    // wave therefore staged the launch's whole LDS, the blocks past the image reading row 0.
     constexpr u32 NCH = RBY / 16;
     constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
     constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
@@ -1187,12 +1186,11 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // lr = x / NCH at physical chunk pc = x % NCH, read from the logical chunk lds_chunk(lr, pc)
     // of A[rows[q0 + lr]] (the XOR is an involution). The row indices of the wave's blocks are
     // loaded once, one per lane, and handed to the block's lanes with v_readlane + select.
-    // Every wave stages exactly MAXB blocks b = w + i NW (the launch's whole LDS: 160 KiB at 1024
-    // threads, 80 KiB at 512), unconditionally: blocks past the image land in its unused tail
-    // (their rows read A row 0). A branch around a block, or any LDS instruction between two
-    // LDS-DMAs (a ds_bpermute hand-out of the row indices did this), makes the compiler wait
-    // (vmcnt(0)) for each LDS-DMA before issuing the next, which serialised the staging
-    // (C2: 12.8 -> 12.0 us once removed).
+    // Wave w stages the image's blocks b = w + i NW < stageBlocks, back to back, by inline-asm
+    // LDS-DMAs (rb_dma16): around the builtin, a branch (skipping a block) or any LDS instruction
+    // between two LDS-DMAs made the compiler wait (vmcnt(0)) for each LDS-DMA before issuing the
+    // next, which serialised the staging (C2: 12.8 -> 12.0 us once removed); until round 5 every
+    // wave therefore staged the launch's whole LDS, the blocks past the image reading row 0.
     constexpr u32 NCH = RBY / 16;
     constexpr u32 NR = NCH >= 64 ? 1 : 64 / NCH;  // rows a block starts (<= 4)
     constexpr u32 MAXB = (NT == 1024 ? 160u : 80u) / NW;
@@ -1671,7 +1669,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     }
 #undef BSMR_RB2
 #undef BSMR_RB
-    // k_sddmm_rb stages a fixed 160 / 80 KiB per workgroup (the image and an unused tail)
+    // the workgroup's LDS: 160 / 80 KiB (the image, the staged-output slots, the batch counter)
     const u32 grid = sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
     hipLaunchKernelGGL(fn, dim3(grid, nb), dim3(L.NT),
                        (L.NT == 1024 ? 160 : 80) * 1024, s, a);
