@@ -61,7 +61,7 @@ __device__ __forceinline__ u32 fslot(u32 r, u32 g) { return (FKC / 8) * r + (g ^
 __device__ __forceinline__ void lds_dma16(const char* g, char* l) {
     const u32 m0 = __builtin_amdgcn_readfirstlane(static_cast<u32>(
         reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)l)));
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
                  : "memory", "m0");
 }
 

@@ -704,6 +704,24 @@ extern "C" int bsmr_check_rphm_arrays(uint32_t M, uint32_t N, uint32_t nnz, cons
         set_error("bsmr_check_rphm_arrays: bad arguments");
         return BSMR_ERR_INVALID;
     }
+    // the checks index per-column and per-entry vectors with S itself: an untrusted S must be a
+    // well-formed CSR first (rowptr non-decreasing from 0 to nnz, every column < N)
+    if (rowptr[0] != 0) {
+        set_error("bsmr_check_rphm_arrays: rowptr[0] != 0");
+        return BSMR_ERR_INVALID;
+    }
+    for (u32 r = 0; r < M; ++r)
+        if (rowptr[r + 1] < rowptr[r] || rowptr[r + 1] > nnz) {
+            set_error("bsmr_check_rphm_arrays: rowptr is not non-decreasing within [0, nnz] at row " +
+                      std::to_string(r));
+            return BSMR_ERR_INVALID;
+        }
+    for (u32 k = 0; k < nnz; ++k)
+        if (colidx[k] >= N) {
+            set_error("bsmr_check_rphm_arrays: colidx[" + std::to_string(k) + "] = " +
+                      std::to_string(colidx[k]) + " is not below N");
+            return BSMR_ERR_INVALID;
+        }
     const u32 P = (R + 15) / 16;
     Checker c(nullptr, delta, verbose);
     Host& h = c.h();

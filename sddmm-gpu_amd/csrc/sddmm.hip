@@ -474,10 +474,10 @@ __device__ __forceinline__ u32 lds_addr(const char* l) {
 template <int AUX>
 __device__ __forceinline__ void rb_dma16(const char* g, const u32 m0) {
     if constexpr (AUX == 2)
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0)
                      : "memory", "m0");
     else
-        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0)
                      : "memory", "m0");
 }
 

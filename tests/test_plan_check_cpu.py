@@ -120,3 +120,25 @@ def test_delta_mismatch_is_caught(capfd):
     err = capfd.readouterr().err
     assert not ok and "does not match delta" in msg
     assert "Error! The col reordering is incorrect!" in err
+
+
+@pytest.mark.parametrize("kind", ["colidx_past_N", "rowptr_decreasing", "rowptr_past_nnz"])
+def test_malformed_csr_is_rejected_before_checking(kind):
+    """bsmr_check_rphm_arrays takes untrusted host arrays: a column index >= N or a rowptr that is
+    not non-decreasing within [0, nnz] is refused with BSMR_ERR_INVALID before any check indexes
+    per-column or per-entry vectors with it (colidx == N + 5 used to write past them)."""
+    M, N, rp, ci = synth.random_rows(200, 300, 20, seed=6)
+    arr = _oracle_arrays(M, N, rp, ci, 0.3, 0.3)
+    rp, ci = rp.astype(np.uint32).copy(), ci.astype(np.uint32).copy()
+    if kind == "colidx_past_N":
+        ci[len(ci) // 2] = N + 5
+        want = "is not below N"
+    elif kind == "rowptr_decreasing":
+        rp[50] = rp[52] + 1
+        want = "rowptr is not non-decreasing"
+    else:
+        rp[10] = len(ci) + 7
+        want = "rowptr is not non-decreasing"
+    with pytest.raises(bsmr.BsmrError) as ei:
+        bsmr.check_rphm_arrays(M, N, rp, ci, arr, 0.3, verbose=False)
+    assert "status 1" in str(ei.value) and want in str(ei.value), str(ei.value)
