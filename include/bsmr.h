@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 11 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 12 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
                               the plan options (no environment reads in the library);
@@ -30,7 +30,10 @@ extern "C" {
                               9: bsmr_tuning.cluster_filter, filter stats;
                               10: bsmr_plan_check, bsmr_check_rphm_arrays, BSMR_ERR_CHECK,
                               bsmr_tuning.pair_min_items, stats rb_pairs;
-                              11: bsmr_tuning.batches, stats rb_batches */
+                              11: bsmr_tuning.batches, stats rb_batches;
+                              12: bsmr_tuning.ptile / ptile_tpi (panel-grouped fp16/bf16 tile
+                              launch), stats ptile_items; removed the dropped experiments'
+                              knobs piece_order, seg_items, sweep* and stats rb_sweep */
 
 typedef enum {
     BSMR_OK = 0,
@@ -89,7 +92,6 @@ typedef struct bsmr_plan bsmr_plan;
  * BSMR_<FIELD> variables (the tools/ A/B scripts) copies them in with bsmr_tuning_from_env. */
 typedef struct {
     uint32_t diag;             /* BSMR_DIAG ablation bits (sddmm.hip; results WRONG); 0 = off */
-    int32_t piece_order;       /* BSMR_PIECE_ORDER: 1 = column order inside an item; -1 = 0 */
     int32_t tile_min_f32;      /* BSMR_TILE_MIN_F32: fp32 tiles with fewer entries run as residual
                                   entries on the row-block launch; -1 = 257 (all demoted) */
     int32_t tile_min_half;     /* BSMR_TILE_MIN_HALF: the same for fp16/bf16; -1 = 128 */
@@ -111,9 +113,6 @@ typedef struct {
                                   -1 = auto */
     int32_t stage_nt;          /* BSMR_STAGE_NT: row-block A staging with the nt cache policy, 0
                                   never, 1 always, -1 auto */
-    int32_t seg_items;         /* BSMR_SEG_ITEMS: 1 = one workgroup item per split (row block,
-                                  column range) segment, cut only to the staged-output capacity;
-                                  -1 = cost-apportioned chunks */
     int32_t rb_rows;           /* BSMR_RB_ROWS: rows per row block of the row-block launch (a
                                   multiple of 16 within 160 KiB of LDS); -1 = by the LDS budget */
     int32_t late_b;            /* BSMR_LATE_B: 1 = row-block phase-0 B columns loaded after the
@@ -132,15 +131,6 @@ typedef struct {
     int32_t out_packed;        /* BSMR_OUT_PACKED: unstaged row-block layouts carry each entry's CSR
                                   position in its metadata word (one 4-byte load per entry instead
                                   of two), 0 never, else whenever nnz <= 2^22; -1 = auto */
-    int32_t sweep;             /* BSMR_SWEEP: range sweep of staged-output row-block layouts (the
-                                  XCD's workgroups walk its column ranges in step),
-                                  0 never, else where it applies; -1 = auto = never (C4 x1
-                                  4.6 vs 3.7 ms) */
-    int32_t sweep_range_kb;    /* BSMR_SWEEP_RANGE_KB: B bytes per sweep column range; -1 = 2048 */
-    float sweep_split;         /* BSMR_SWEEP_SPLIT: largest sweep task as a multiple of the mean;
-                                  < 0 = 1.5 */
-    int32_t sweep_slack;       /* BSMR_SWEEP_SLACK: steps a workgroup may run ahead of its XCD's
-                                  slowest; -1 = 1 */
     int32_t cluster_filter;    /* BSMR_CLUSTER_FILTER: bound every pair's similarity on the matrix
                                   cores before the clustering chain and skip the pairs that cannot
                                   reach alpha (same permutation), 0 never, 1 when
@@ -154,6 +144,11 @@ typedef struct {
                                   pieces to waves in batches from an LDS counter instead of fixed
                                   phases; 0 never, 1 always, -1 = auto (512-byte rows, items of
                                   >= 2 pieces per row-group) */
+    int32_t ptile;             /* BSMR_PTILE: panel-grouped tile launch for fp16/bf16 K in {64, 128,
+                                  256, 512} (every BSMR tile on MFMA, a panel's A rows staged once
+                                  per item): 0 never, 1 whenever dtype and K allow, -1 = auto
+                                  (tile-dominated plans, e.g. 16 x 16 block masks) */
+    int32_t ptile_tpi;         /* BSMR_PTILE_TPI: tiles per panel-tile item, 1..64; -1 = 8 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -248,8 +243,8 @@ typedef struct {
     /* bit i set: row-block layout i (as rb_rows) uses original-order row blocks (banded patterns
      * whose reordering scatters the band) */
     uint32_t rb_orig_rows;
-    /* bit i set: row-block layout i runs as a range sweep (k_sddmm_rb_sweep, bsmr_tuning.sweep) */
-    uint32_t rb_sweep;
+    /* panel-grouped tile launch (bsmr_tuning.ptile): item slots of its list, 0 = not built */
+    uint32_t ptile_items;
     /* clustering candidate filter (bsmr_tuning.cluster_filter): 1 when it ran, and its time
      * (included in row_reorder_ms) */
     uint32_t cluster_filter_used;

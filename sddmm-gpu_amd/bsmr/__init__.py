@@ -40,17 +40,16 @@ class BsmrError(RuntimeError):
 
 class Tuning(C.Structure):
     """bsmr_tuning: launch-layout knobs (include/bsmr.h). "auto" = -1 (diag 0)."""
-    _fields_ = [("diag", C.c_uint32), ("piece_order", C.c_int32), ("tile_min_f32", C.c_int32),
+    _fields_ = [("diag", C.c_uint32), ("tile_min_f32", C.c_int32),
                 ("tile_min_half", C.c_int32), ("piece_max", C.c_int32),
                 ("piece_weight", C.c_float), ("shard_piece_weight", C.c_float),
                 ("dense_min", C.c_float), ("orig_rows", C.c_int32), ("orig_contig", C.c_int32),
                 ("dense_ks", C.c_int32), ("dense_ns", C.c_int32), ("out_staged", C.c_int32),
-                ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32), ("seg_items", C.c_int32),
+                ("l2_range_kb", C.c_int32), ("stage_nt", C.c_int32),
                 ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
-                ("item_sched", C.c_int32), ("out_packed", C.c_int32), ("sweep", C.c_int32),
-                ("sweep_range_kb", C.c_int32), ("sweep_split", C.c_float), ("sweep_slack", C.c_int32),
+                ("item_sched", C.c_int32), ("out_packed", C.c_int32),
                 ("cluster_filter", C.c_int32), ("pair_min_items", C.c_int32),
-                ("batches", C.c_int32)]
+                ("batches", C.c_int32), ("ptile", C.c_int32), ("ptile_tpi", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -82,7 +81,7 @@ class PlanStats(C.Structure):
                 ("rb_pieces", C.c_uint32 * 5), ("rb_entries", C.c_uint32 * 5),
                 ("rb_tiles", C.c_uint32 * 5), ("rb_work_items", C.c_uint32 * 5),
                 ("dense_sampled_tiles", C.c_uint32), ("rb_orig_rows", C.c_uint32),
-                ("rb_sweep", C.c_uint32), ("cluster_filter_used", C.c_uint32),
+                ("ptile_items", C.c_uint32), ("cluster_filter_used", C.c_uint32),
                 ("cluster_filter_ms", C.c_float), ("rb_pairs", C.c_uint32),
                 ("rb_batches", C.c_uint32)]
 
@@ -124,7 +123,7 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 11  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 12  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -247,9 +246,10 @@ def tuning_from_env(env=None):
         v = env.get(TUNING_ENV[f])
         if v is None:
             continue
-        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "sweep", "cluster_filter"):  # tri-state: "0" never, "1" always, else auto
+        if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "cluster_filter",
+                 "batches", "ptile"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
-        elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap", "sweep_split"):
+        elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap"):
             out[f] = float(v)
         else:
             out[f] = int(v)

@@ -25,22 +25,20 @@ extern "C" void bsmr_plan_options_default(bsmr_plan_options* o) {
 
 extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->diag = 0;
-    t->piece_order = t->tile_min_f32 = t->tile_min_half = t->piece_max = -1;
+    t->tile_min_f32 = t->tile_min_half = t->piece_max = -1;
     t->piece_weight = t->shard_piece_weight = t->dense_min = -1.0f;
     t->orig_rows = t->orig_contig = t->dense_ks = t->dense_ns = t->out_staged = -1;
     t->l2_range_kb = -1;
     t->stage_nt = -1;
-    t->seg_items = -1;
     t->rb_rows = -1;
     t->late_b = -1;
     t->item_cap = -1.0f;
     t->item_sched = -1;
     t->out_packed = -1;
-    t->sweep = t->sweep_range_kb = t->sweep_slack = -1;
-    t->sweep_split = -1.0f;
     t->cluster_filter = -1;
     t->pair_min_items = -1;
     t->batches = -1;
+    t->ptile = t->ptile_tpi = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -68,7 +66,6 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
         t->diag = static_cast<uint32_t>(std::atoi(v));
         ++n;
     }
-    geti("BSMR_PIECE_ORDER", t->piece_order);
     geti("BSMR_TILE_MIN_F32", t->tile_min_f32);
     geti("BSMR_TILE_MIN_HALF", t->tile_min_half);
     geti("BSMR_PIECE_MAX", t->piece_max);
@@ -82,19 +79,16 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     get3("BSMR_OUT_STAGED", t->out_staged);
     geti("BSMR_L2_RANGE_KB", t->l2_range_kb);
     get3("BSMR_STAGE_NT", t->stage_nt);
-    geti("BSMR_SEG_ITEMS", t->seg_items);
     geti("BSMR_RB_ROWS", t->rb_rows);
     geti("BSMR_LATE_B", t->late_b);
     getf("BSMR_ITEM_CAP", t->item_cap);
     get3("BSMR_ITEM_SCHED", t->item_sched);
     get3("BSMR_OUT_PACKED", t->out_packed);
-    get3("BSMR_SWEEP", t->sweep);
-    geti("BSMR_SWEEP_RANGE_KB", t->sweep_range_kb);
-    getf("BSMR_SWEEP_SPLIT", t->sweep_split);
-    geti("BSMR_SWEEP_SLACK", t->sweep_slack);
     get3("BSMR_CLUSTER_FILTER", t->cluster_filter);
     geti("BSMR_PAIR_MIN_ITEMS", t->pair_min_items);
     get3("BSMR_BATCHES", t->batches);
+    get3("BSMR_PTILE", t->ptile);
+    geti("BSMR_PTILE_TPI", t->ptile_tpi);
     return n;
 }
 
@@ -129,7 +123,6 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
     }
     if (const bsmr_tuning* t = o.tuning) {  // launch-layout knobs; "auto" keeps the defaults
         p.diag = t->diag;
-        if (t->piece_order >= 0) p.piece_order = static_cast<u32>(t->piece_order);
         if (t->tile_min_f32 >= 0) p.tile_min_f32 = static_cast<u32>(t->tile_min_f32);
         if (t->tile_min_half >= 0) p.tile_min_half = static_cast<u32>(t->tile_min_half);
         if (t->piece_max >= 0) p.piece_max = std::min<u32>(RB_PIECE_MAX, std::max(1, t->piece_max));
@@ -143,19 +136,16 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->out_staged >= 0) p.out_staged = t->out_staged ? 1 : 0;
         if (t->out_packed >= 0) p.out_packed = t->out_packed ? 1 : 0;
         if (t->stage_nt >= 0) p.stage_nt = t->stage_nt ? 1 : 0;
-        if (t->seg_items >= 0) p.seg_items = t->seg_items;
         if (t->rb_rows > 0) p.rb_rows_force = t->rb_rows;
         if (t->late_b >= 0) p.late_b = t->late_b;
         if (t->item_cap >= 0) p.item_cap = t->item_cap;
         if (t->item_sched >= 0)
             p.item_cost_cuts = p.item_lpt = p.small_sparse_rb = t->item_sched != 0;
-        if (t->sweep >= 0) p.sweep_mode = t->sweep ? 1 : 0;
-        if (t->sweep_range_kb >= 0) p.sweep_range_kb = static_cast<u32>(std::max(64, t->sweep_range_kb));
-        if (t->sweep_split >= 0) p.sweep_split = std::max(0.25f, t->sweep_split);
-        if (t->sweep_slack >= 0) p.sweep_slack = static_cast<u32>(t->sweep_slack);
         if (t->cluster_filter >= 0) p.cluster_filter = t->cluster_filter ? 1 : 0;
         if (t->pair_min_items >= 0) p.pair_min_items = static_cast<u32>(t->pair_min_items);
         if (t->batches >= 0) p.batches = t->batches ? 1 : 0;
+        if (t->ptile >= 0) p.ptile_mode = t->ptile ? 1 : 0;
+        if (t->ptile_tpi > 0) p.ptile_tpi = static_cast<u32>(std::min(64, t->ptile_tpi));
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -373,11 +363,11 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_tiles[i] = L.rowBytes ? L.nTilesKept : 0;
         s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
         if (L.rowBytes && L.orig) s->rb_orig_rows |= 1u << i;
-        if (L.rowBytes && L.sweep) s->rb_sweep |= 1u << i;
         if (L.rowBytes && rb_uses_pairs(p, L)) s->rb_pairs |= 1u << i;
         if (L.rowBytes && L.dynBatches) s->rb_batches |= 1u << i;
     }
     s->dense_sampled_tiles = p.dense.built ? p.dense.nonempty : 0;
+    s->ptile_items = p.ptile.built ? p.ptile.nItems : 0;
     return BSMR_OK;
 }
 

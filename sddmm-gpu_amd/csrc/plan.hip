@@ -1759,12 +1759,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // that XCD's L2 by the items before it (graph matrices: B is gathered once per row block and
     // column run, from L2 instead of the Infinity Cache)
     constexpr u32 CM = (1u << 22) - 1;
-    // range sweep (sddmm.hip k_sddmm_rb_sweep): staged output over reordered rows of >= 256 bytes
-    // with no kept MFMA tile; the XCD's column share in ranges of sweep_range_kb (2 MiB, or the
-    // user's l2_range_kb), walked by all of the XCD's workgroups in step (BSMR_DIAG & 262144: off)
-    const bool sweepWanted = stagedWanted && !orig && hkept.empty() && rowBytes >= 256 && sweep_mode != 0 &&
-                             !(diag & 262144) && n > 0;
-    const u32 rangeKb = sweepWanted && !l2_range_user ? sweep_range_kb : l2Kb;
+    const u32 rangeKb = l2Kb;
     const u32 m = std::max<u32>(1, static_cast<u32>(std::ceil(
         static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(rangeKb) * 1024.0))));
     const u32 NCR = XCD_BUCKETS * m;
@@ -1980,15 +1975,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             for (u32 b = 0; b < nRB; ++b)
                 c[static_cast<size_t>(j) * nRB + b] =
                     split[b] ? cost[static_cast<size_t>(b) * NCR + x * m + j] : 0.0;
-        // one_item_per_segment: every (row block, range) segment is one item (cut only to the
-        // staged-output capacity), so no A image is staged twice for one segment; the XCD lists
-        // then differ in length by their segment counts
-        u32 qx = qEach;
-        if (seg_items == 1) {
-            qx = 0;
-            for (double v : c) qx += v > 0;
-        }
-        const std::vector<u32> nch = apportion(c, qx, seg_items == 1 ? 0.0 : capv);
+        const std::vector<u32> nch = apportion(c, qEach, capv);
         for (u32 j = 0; j < m; ++j)
             for (u32 b = 0; b < nRB; ++b) {
                 const size_t i = static_cast<size_t>(b) * NCR + x * m + j;
@@ -2106,105 +2093,6 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     lap("chunks");
     std::vector<uint4> items;
     std::vector<u32> ends;
-    // range sweep: per XCD, W = perBucket persistent workgroups (one per CU). Every row block
-    // with entries in the XCD's share is a task (heavy blocks several tasks, each 1/h of every
-    // range's entries, so no task exceeds sweep_split x the mean); tasks go to rounds of W by
-    // descending cost, each round's tasks to the workgroups least loaded so far. A task stages
-    // its image once and walks the XCD's m ranges in order, one item per outCap results; its
-    // items carry the step r m + k (round r, range k) at which the workgroups of the XCD meet
-    // (sddmm.hip k_sddmm_rb_sweep: a bounded wait, locality only)
-    const bool sweep = sweepWanted && staged && m >= 2 && NT == 1024;
-    std::vector<u32> wgStart, itemStep;
-    u32 sweepSteps = 0;
-    if (sweep) {
-        const u32 W = perBucket;
-        // cost cuts of an entry range into h parts (entries + piece_weight per column-run start)
-        auto part_cuts = [&](u32 e0, u32 ne, u32 h) {
-            std::vector<u32> pc(h + 1, e0 + ne);
-            pc[0] = e0;
-            if (h > 1) {
-                double tot = 0;
-                u32 run = 0;
-                for (u32 e = e0; e < e0 + ne; ++e) {
-                    const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
-                    run = start ? 1 : run + 1;
-                    tot += 1.0 + (start ? piece_weight : 0.0);
-                }
-                double acc = 0;
-                u32 k = 1;
-                run = 0;
-                for (u32 e = e0; e < e0 + ne && k < h; ++e) {
-                    const bool start = e == e0 || (hmeta[e] & CM) != (hmeta[e - 1] & CM) || run >= piece_max;
-                    run = start ? 1 : run + 1;
-                    while (k < h && acc >= tot * k / h) pc[k++] = e;
-                    acc += 1.0 + (start ? piece_weight : 0.0);
-                }
-            }
-            return pc;
-        };
-        wgStart.reserve(static_cast<size_t>(XCD_BUCKETS) * W + 1);
-        for (u32 x = 0; x < XCD_BUCKETS; ++x) {
-            struct Task {
-                u32 b, j, h;
-                double c;
-            };
-            std::vector<Task> tasks;
-            std::vector<double> tc(nRB, 0.0);
-            double tot = 0;
-            u32 nz = 0;
-            for (u32 b = 0; b < nRB; ++b) {
-                for (u32 k = 0; k < m; ++k) tc[b] += cost[static_cast<size_t>(b) * NCR + x * m + k];
-                tot += tc[b];
-                nz += tc[b] > 0;
-            }
-            const double mean = nz ? tot / nz : 0.0;
-            for (u32 b = 0; b < nRB; ++b) {
-                if (tc[b] <= 0) continue;
-                const u32 h = std::max<u32>(1, static_cast<u32>(std::ceil(tc[b] / (sweep_split * mean))));
-                for (u32 j = 0; j < h; ++j) tasks.push_back({b, j, h, tc[b] / h});
-            }
-            std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.c > b.c; });
-            const u32 R = static_cast<u32>((tasks.size() + W - 1) / W);
-            sweepSteps = std::max(sweepSteps, R * m);
-            std::vector<double> load(W, 0.0);
-            std::vector<std::vector<std::pair<u32, u32>>> prog(W);  // (round, task)
-            std::vector<u32> byLoad(W);
-            for (u32 r = 0; r < R; ++r) {
-                for (u32 w = 0; w < W; ++w) byLoad[w] = w;
-                std::stable_sort(byLoad.begin(), byLoad.end(), [&](u32 a, u32 b) { return load[a] < load[b]; });
-                for (u32 q = 0; q < W && r * W + q < tasks.size(); ++q) {
-                    const u32 t = r * W + q, w = byLoad[q];
-                    prog[w].push_back({r, t});
-                    load[w] += tasks[t].c;
-                }
-            }
-            for (u32 w = 0; w < W; ++w) {
-                wgStart.push_back(static_cast<u32>(items.size()));
-                for (const auto& [r, t] : prog[w]) {
-                    const Task& T = tasks[t];
-                    bool first = true;
-                    for (u32 k = 0; k < m; ++k) {
-                        const size_t i = static_cast<size_t>(T.b) * NCR + x * m + k;
-                        const u32 ne = se1[i] - se0[i];
-                        if (!ne) continue;
-                        const std::vector<u32> pc = part_cuts(se0[i], ne, T.h);
-                        const u32 a0 = pc[T.j], a1 = pc[T.j + 1], len = a1 - a0;
-                        if (!len) continue;
-                        const u32 parts = (len + outCap - 1) / outCap;
-                        for (u32 q = 0; q < parts; ++q) {
-                            const u32 ea = a0 + static_cast<u32>(static_cast<u64>(len) * q / parts);
-                            const u32 eb = a0 + static_cast<u32>(static_cast<u64>(len) * (q + 1) / parts);
-                            items.push_back(make_uint4(T.b, 0, 0, ea));
-                            ends.push_back(eb);
-                            itemStep.push_back(((r * m + k) << 1) | (first ? 1u : 0u));
-                            first = false;
-                        }
-                    }
-                }
-            }
-        }
-        wgStart.push_back(static_cast<u32>(items.size()));
-    } else {
     size_t nmax = 0;
     for (const auto& l : lists) nmax = std::max(nmax, l.size());
     // staged layouts: an even number of list positions, so the launch can pair them (k_sddmm_rb)
@@ -2216,16 +2104,12 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             items[j * XCD_BUCKETS + x] = lists[x][j];
             ends[j * XCD_BUCKETS + x] = lends[x][j];
         }
-    }
     lap("items");
     // column-run pieces: each item's entries [e0, e1) cut at column changes and every
     // piece_max (<= RB_PIECE_MAX) entries; piece {first entry, column | (length - 1) << 22}. A workgroup's NG
     // row-groups take one piece each per phase, so phase ph runs the item's pieces
-    // [ph NG, (ph + 1) NG). Longest first, so the 16 row-groups of a wave get pieces of similar
-    // length: over the whole item (piece_order 0), or inside column windows of one phase
-    // (piece_order 1: all items of an XCD would sweep their column range together)
-    const u32 G = rowBytes >= 2048 ? 16 : rowBytes >= 1024 ? 8 : 4;  // sddmm.hip RowGeom (128..512: 4)
-    const u32 NG = piece_order == 1 ? NT / G : 0xFFFFFFFFu;  // sort window
+    // [ph NG, (ph + 1) NG). Longest first over the whole item, so the 16 row-groups of a wave get
+    // pieces of similar length
     std::vector<uint2> ient(items.size());
     for (size_t i = 0; i < items.size(); ++i)
         ient[i] = make_uint2(items[i].w, (items[i].y == items[i].z && items[i].w == ends[i]) ? 0u
@@ -2243,9 +2127,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                 mine.push_back(make_uint2(e, col | ((f - e - 1) << 22)));
                 e = f;
             }
-            for (size_t w0 = 0; w0 < mine.size(); w0 += NG)
-                std::stable_sort(mine.begin() + w0, mine.begin() + std::min<size_t>(mine.size(), w0 + NG),
-                                 [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
+            std::stable_sort(mine.begin(), mine.end(),
+                             [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
         }
     });
     std::vector<size_t> poff(items.size() + 1, 0);
@@ -2391,9 +2274,6 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         L.outPacked = true;
     }
     lap("staged");
-    // the sweep kernel stores by runs only; without a run table the items (independent, in any
-    // order) run on k_sddmm_rb, one workgroup each
-    L.sweep = sweep && L.outRuns;
     // dynamic piece batches (Plan::batches; kernels for rows of <= 512 B): after its first batch
     // of 64 / G pieces a wave takes the next from an LDS counter, which balances the waves of
     // items with several pieces per row-group. Measured (profiles/r05bt, forced on against off):
@@ -2404,18 +2284,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     {
         const u32 NGl = NT / 4;  // row-groups (G = 4 for rows of <= 512 B)
         const double perItem = L.nWorkItems ? static_cast<double>(pieces.size()) / L.nWorkItems : 0.0;
-        L.dynBatches = rowBytes <= 512 && !L.sweep &&
+        L.dynBatches = rowBytes <= 512 &&
                        (batches == 1 || (batches < 0 && rowBytes == 512 && perItem >= batch_min_phases * NGl));
-    }
-    L.sweepW = L.sweep ? perBucket : 0;
-    L.sweepSteps = L.sweep ? sweepSteps : 0;
-    L.wgStart.release();
-    L.itemStep.release();
-    L.sweepDone.release();
-    if (L.sweep) {
-        BSMR_CHECK(L.wgStart.upload(wgStart.data(), wgStart.size(), s));
-        BSMR_CHECK(L.itemStep.upload(itemStep.data(), std::max<size_t>(itemStep.size(), 1), s));
-        BSMR_CHECK(L.sweepDone.alloc(static_cast<size_t>(XCD_BUCKETS) * std::max<u32>(sweepSteps, 1)));
     }
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
     BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));

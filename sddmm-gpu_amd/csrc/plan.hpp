@@ -23,6 +23,9 @@ int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype,
 // fp16/bf16 dense-sampled launch (sddmm_dense.hip): K a multiple of 64
 int launch_dense(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
                  hipStream_t s, u32 nb = 1);
+// fp16/bf16 panel-grouped tile launch (sddmm_half.hip): K in {64, 128, 256, 512}; mode as above
+int launch_ptile(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
+                 u32 mode, hipStream_t s, u32 nb = 1);
 
 // clustering candidate filter (cluster_filter.hip): the bit triangle of pairs (leader q,
 // position p > q) whose similarity bound may reach alpha; W = words per full row
@@ -53,9 +56,6 @@ struct Plan {
     // (144 KiB, 2 MiB) -> 1.128 ms at (120 KiB, 4 MiB); C3 unchanged (72.9-73.2 us)
     u32 rb_lds_kb_staged = 120, l2_range_kb_staged = 4096;
     u32 diag = 0;  // BSMR_DIAG profiling ablations (wrong results; never set in normal use)
-    // row-block piece order inside an item (tuning experiments: BSMR_PIECE_ORDER): 0 = longest
-    // first over the whole item, 1 = column windows of one phase, longest first inside
-    u32 piece_order = 0;
     // L2 budget of one column range of the row-block layout (KiB; BSMR_L2_RANGE_KB)
     u32 l2_range_kb = 2048;
     bool l2_range_user = false;  // BSMR_L2_RANGE_KB given: then also for staged layouts
@@ -81,8 +81,6 @@ struct Plan {
     // A staging with the nt cache policy (BSMR_STAGE_NT: 0 never, 1 always, else auto = staged
     // output layouts when stage_nt_auto)
     int stage_nt = -1;
-    // BSMR_SEG_ITEMS: 1 = one item per split (row block, column range) segment
-    int seg_items = -1;
     int rb_rows_force = -1;  // BSMR_RB_ROWS: rows per row block (tuning / experiments)
     // BSMR_LATE_B: phase-0 B loads after the staging barrier (0 = behind the LDS-DMAs, else on).
     // Measured (profiles/r03d/ab_lateb): C2 11.05 -> 10.86 us, C3 72.0 -> 68.9, C4 x0.5 1.012 ->
@@ -94,12 +92,6 @@ struct Plan {
     double item_cap = -1.0;  // < 0: auto (build_rowblock_layout), 0: no cap
     bool item_cost_cuts = true, item_lpt = true;
     double item_fixed = 1024.0;
-    // range sweep of staged layouts (k_sddmm_rb_sweep): 0 off, else on; B bytes per range; the
-    // largest task as a multiple of the mean task cost; steps a workgroup may run ahead
-    int sweep_mode = 0;  // off by default: C4 x1 4.61 vs 3.72 ms (profiles/r04v, r04w)
-    u32 sweep_range_kb = 2048;
-    double sweep_split = 1.5;
-    u32 sweep_slack = 1;
     // sparse-row patterns with fewer row blocks than slots: one block per workgroup slot
     bool small_sparse_rb = true;
     bool stage_nt_auto = false;
@@ -198,12 +190,6 @@ struct Plan {
         // per result, and sortedPos is released
         bool outRuns = false;
         DevBuf<uint2> runs, itemRuns;
-        // range sweep (k_sddmm_rb_sweep): workgroup p = x W + w runs items [wgStart[p],
-        // wgStart[p + 1]); itemStep[i] = step << 1 | first item of its task (stages the image);
-        // sweepDone: per XCD and step, the workgroups that have left the step (reset per launch)
-        bool sweep = false;
-        u32 sweepW = 0, sweepSteps = 0;
-        DevBuf<u32> wgStart, itemStep, sweepDone;
         DevBuf<uint4> items;
         DevBuf<u32> itemEnd;
         DevBuf<uint2> pieces;  // {first entry, column | (length - 1) << 22}
@@ -280,6 +266,18 @@ struct Plan {
     int dense_ks = 0;
     int dense_ns = 2;  // BSMR_DENSE_NS: LDS stages of the eight-wave dense launch (2..5)
     int build_dense_layout() const;
+
+    // panel-grouped tile launch (sddmm_half.hip k_sddmm_ptile): tile-dominated fp16/bf16 plans,
+    // K in {64, 128, 256, 512}; items {panel, first tile, tiles <= tpi, 0} in launch order
+    struct PtileLayout {
+        bool built = false;
+        u32 tpi = 0, nItems = 0, nListed = 0;
+        DevBuf<uint4> items;
+    };
+    mutable PtileLayout ptile;
+    int ptile_mode = -1;  // BSMR_PTILE: 0 never, 1 whenever it applies, -1 auto
+    u32 ptile_tpi = 8;    // BSMR_PTILE_TPI: tiles per item
+    int build_ptile_layout(u32 tpi) const;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);
     int build_columns();

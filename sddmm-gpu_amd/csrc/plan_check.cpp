@@ -38,6 +38,7 @@
 namespace bsmr {
 
 bool sddmm_uses_dense(const Plan& p, u32 K, int dtype);  // sddmm.hip
+bool sddmm_uses_ptile(const Plan& p, u32 K, int dtype);  // sddmm.hip
 
 namespace {
 
@@ -297,6 +298,16 @@ public:
                 if (!p_.dense.built) BSMR_CHECK(p_.build_dense_layout());
             }
             *ok = dense_layout();
+            return BSMR_OK;
+        }
+        if (sddmm_uses_ptile(p_, K, dtype)) {
+            {
+                std::lock_guard<std::mutex> g(p_.layout_mu);
+                if (!p_.ptile.built || p_.ptile.tpi != p_.ptile_tpi) BSMR_CHECK(p_.build_ptile_layout(p_.ptile_tpi));
+            }
+            bool r = false;
+            BSMR_CHECK(ptile_layout(&r));
+            *ok = r;
             return BSMR_OK;
         }
         const Plan::RowBlockLayout* L = nullptr;
@@ -624,6 +635,32 @@ private:
     }
 
     // column-major launch (k_sddmm_f32 / k_sddmm_half): every tile + residual slots
+    // the panel-grouped tile launch: every tile id in exactly one item, inside the item's panel
+    // (its A rows are the panel's 16 reordered rows), at most tpi per item; then the residual
+    // slots as in the column-major launch
+    int ptile_layout(bool* ok) {
+        const Plan& p_ = *pp_;
+        std::vector<uint4> items;
+        BSMR_CHECK(p_.ptile.items.download(items, p_.stream));
+        items.resize(p_.ptile.nItems);
+        *ok = false;
+        const u32 nt = static_cast<u32>(h_.bv.size() / TILE);
+        std::vector<uint8_t> thit(std::max<u32>(nt, 1), 0);
+        if (p_.ptile.nItems % XCD_BUCKETS)
+            return layout_fail(fmt("panel-tile launch: %u item slots, not a multiple of 8", p_.ptile.nItems)), BSMR_OK;
+        for (u32 i = 0; i < p_.ptile.nItems; ++i) {
+            const uint4 it = items[i];
+            if (it.z == 0) continue;
+            if (it.x >= h_.P || it.z > p_.ptile.tpi || it.y < h_.bo[it.x] || it.y + it.z > h_.bo[it.x + 1])
+                return layout_fail(fmt("panel-tile item %u {panel %u, tile %u, %u tiles} outside its panel", i, it.x, it.y, it.z)), BSMR_OK;
+            for (u32 t = it.y; t < it.y + it.z; ++t)
+                if (thit[t]++) return layout_fail(fmt("panel-tile: tile %u in two items", t)), BSMR_OK;
+        }
+        for (u32 t = 0; t < nt; ++t)
+            if (!thit[t]) return layout_fail(fmt("panel-tile: tile %u in no item", t)), BSMR_OK;
+        return cm_layout(ok);
+    }
+
     int cm_layout(bool* ok) {
         const Plan& p_ = *pp_;
         hipStream_t s = p_.stream;

@@ -428,14 +428,6 @@ struct RbArgs {
     const uint2* runs;
     const uint2* itemRuns;
     u32 pairs;  // 1: each workgroup runs list positions 2j and 2j + 1 of its XCD (see k_sddmm_rb)
-    // range sweep (RowBlockLayout::sweep, k_sddmm_rb_sweep): workgroup x W + w runs items
-    // [wgStart[x W + w], wgStart[x W + w + 1]); itemStep[i] = step << 1 | restage; sweepDone[x S + g]
-    // counts the workgroups of XCD x past step g (S = sweepSteps); a workgroup enters step g once
-    // sweepDone[x S + g - slack - 1] reached W, or after a bounded wait
-    const u32* wgStart;
-    const u32* itemStep;
-    u32* sweepDone;
-    u32 sweepW, sweepSteps, sweepSlack;
     unsigned long long* trace;  // BSMR_DIAG & 32 timeline (see trace_wave)
     u32 diag;                   // profiling ablations (BSMR_DIAG); always 0 in normal use
     unsigned long long bA, bB, bP;  // batched launch: A, B byte strides, P element stride
@@ -845,8 +837,8 @@ template <int DT, int RBY, int NT, int OM, bool DYN = false>
 __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx, const bool prestaged,
                                         const u32 next) {
     // OM (output mode): 0 = one store per entry (a.outLds == 0), 1 = staged output (slots in
-    // LDS, written per item in CSR order), 2 = staged output by runs in pairs (PAIR), 3 = staged
-    // output without kept tiles, trace or ablations (the range sweep, LEAN)
+    // LDS, written per item in CSR order), 2 = staged output by runs in pairs (PAIR; LEAN: no
+    // kept tiles, trace or ablations)
     constexpr bool PAIR = OM == 2, STAGED = OM != 0, LEAN = OM >= 2;
     using Geo = RowGeom<RBY>;
     constexpr u32 G = Geo::G, NC = Geo::NC;  // lanes per entry, chunks per lane
@@ -884,7 +876,7 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
     }
     const u32 q0 = a.qbase + it.x * a.RB;
     u32 tid = threadIdx.x;
-    // LEAN (a loop of items per workgroup): the thread-derived values are recomputed per item
+    // LEAN (two items per workgroup): the thread-derived values are recomputed per item
     // rather than hoisted out of the caller's loop, where they would hold VGPRs across it
     if constexpr (LEAN) asm volatile("" : "+v"(tid));
     const u32 w = tid >> 6, sub = tid % G, j = (tid & 63) / G;
@@ -1408,68 +1400,10 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
         rb_item<DT, RBY, NT, 2, DYN>(a, As, i0 + XCD_BUCKETS, true, NO_ITEM);
 }
 
-// the longest a workgroup waits for its XCD's slowest workgroup to leave a step (s_memrealtime
-// ticks, 100 MHz): the wait only keeps the XCD's workgroups inside a window of column ranges (B
-// lines shared in L2); past it the workgroup goes on, so no step ever depends on co-residency
-constexpr u32 SWEEP_WAIT_TICKS = 3000;  // 30 us
-
-// Range sweep (staged output, Plan::build_rowblock_layout): the XCD's W workgroups (one per CU)
-// each run a list of tasks; a task stages its row block's image once and walks the XCD's column
-// ranges in order, one item per staged-output load. Entering a later step, a workgroup counts
-// itself out of the steps before it and waits (bounded) until every workgroup of its XCD has
-// left step g - slack - 1, so the XCD's L2 holds the B columns of at most slack + 1 ranges at a
-// time instead of every range the XCD's items happen to be in
-// the workgroup leaves steps [from, to) of its XCD, then waits (bounded) until every workgroup
-// of the XCD has left step to - slack - 1 (thread 0; the caller's barrier holds the others)
-__device__ __forceinline__ void sweep_leave(const RbArgs& a, const u32 from, const u32 to) {
-    if (threadIdx.x != 0) return;
-    // (the counters' address is recomputed here: fewer SGPRs live across the items)
-    u32* done = a.sweepDone + static_cast<size_t>(blockIdx.x % XCD_BUCKETS) * a.sweepSteps;
-    for (u32 k = from; k < to; ++k)
-        __hip_atomic_fetch_add(done + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (to < a.sweepSteps && to > a.sweepSlack) {
-        const u32* gate = done + (to - a.sweepSlack - 1);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.sweepW &&
-               __builtin_amdgcn_s_memrealtime() - t0 < SWEEP_WAIT_TICKS)
-            __builtin_amdgcn_s_sleep(2);
-    }
-}
-
-template <int DT, int RBY, int NT>
-__global__ __launch_bounds__(NT, 4) void k_sddmm_rb_sweep(RbArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char AsB[];
-    char* As = AsB;
-    if (blockIdx.y) {  // batch b (its workgroups share the counters: they then only gate earlier)
-        a.A += blockIdx.y * a.bA;
-        a.B += blockIdx.y * a.bB;
-        a.P += blockIdx.y * a.bP;
-    }
-    const u32 pw = (blockIdx.x % XCD_BUCKETS) * a.sweepW + blockIdx.x / XCD_BUCKETS;
-    const u32 i1 = __builtin_amdgcn_readfirstlane(a.wgStart[pw + 1]);
-    u32 g = 0;  // the workgroup's step: it has counted itself out of every step before it
-    for (u32 i = __builtin_amdgcn_readfirstlane(a.wgStart[pw]); i < i1; ++i) {
-        const u32 st = __builtin_amdgcn_readfirstlane(a.itemStep[i]);
-        const u32 step = st >> 1;
-        const bool restage = (st & 1) != 0;
-        if (step > g) {
-            __syncthreads();  // the previous item is done (its slots and image read)
-            sweep_leave(a, g, step);  // and (bounded) wait until the XCD has left step - slack - 1
-            g = step;
-            __syncthreads();
-        } else if (restage) {
-            __syncthreads();  // no wave still reads the previous image or its slots
-        }
-        rb_item<DT, RBY, NT, 3>(a, As, i, !restage, NO_ITEM);
-    }
-    sweep_leave(a, g, a.sweepSteps);
-}
-
 template <int DT, int RBY>
-void (*pick_rb(const u32 NT, const bool pairs, const bool sweep, const bool dyn))(RbArgs) {
+void (*pick_rb(const u32 NT, const bool pairs, const bool dyn))(RbArgs) {
     // (dynamic batches: rows of <= 512 B, RowBlockLayout::dynBatches)
     if constexpr (RBY >= 256) {  // (launch_rb enables pairs from 512-byte rows)
-        if (sweep && NT == 1024) return k_sddmm_rb_sweep<DT, RBY, 1024>;
         if (pairs) {
             if constexpr (RBY <= 512)
                 if (dyn) return NT == 1024 ? k_sddmm_rb_pair<DT, RBY, 1024, true> : k_sddmm_rb_pair<DT, RBY, 512, true>;
@@ -1573,6 +1507,17 @@ bool use_dense(const Plan& p, u32 K, int dtype) {
            static_cast<double>(p.nnz) >= static_cast<double>(p.dense_min) * p.M * static_cast<double>(p.N);
 }
 
+// tile-dominated fp16/bf16 plans (16 x 16 block masks: residual under a quarter of the work) with
+// K in {64, 128, 256, 512}: the panel-grouped tile launch (sddmm_half.hip k_sddmm_ptile), every
+// BSMR tile on MFMA with the panel's A rows staged once per item (BSMR_PTILE = 1: whenever the
+// dtype and K allow, also beside a large residual; 0: never)
+bool use_ptile(const Plan& p, u32 K, int dtype) {
+    if (dtype == BSMR_F32 || p.ptile_mode == 0 || !p.use_rowblock || p.force_rowblock) return false;
+    if ((K != 64 && K != 128 && K != 256 && K != 512) || p.numDenseTiles == 0) return false;
+    return p.ptile_mode == 1 ||
+           static_cast<u64>(p.nres) * 4 < static_cast<u64>(p.numDenseTiles) * 16;
+}
+
 // the row-block layout of panels [pa, pb) for slot's row size (built on first use)
 int get_rb_layout(const Plan& p, int slot, int dtype, u32 pa, u32 pb,
                   std::shared_ptr<const Plan::RowBlockLayout>* out) {
@@ -1628,19 +1573,6 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     // 108.9; C4 (8-30 K items) gains (x0.5 1.029 -> 0.984 ms), C3, mycielskian16 K = 128 and
     // 1-2 KiB rows are neutral (profiles/r04zt, r04zw)
     a.pairs = mode == 3 && rb_uses_pairs(p, L) ? 1u : 0u;
-    // the range sweep's per-XCD step counters serve one launch of one batch: batched launches run
-    // a sweep layout's items as independent workgroups on k_sddmm_rb (items are self-contained)
-    const bool sweep = L.sweep && nb == 1;
-    if (sweep) {
-        a.pairs = 0;
-        a.wgStart = L.wgStart.data();
-        a.itemStep = L.itemStep.data();
-        a.sweepDone = L.sweepDone.data();
-        a.sweepW = L.sweepW;
-        a.sweepSteps = L.sweepSteps;
-        a.sweepSlack = p.sweep_slack;
-        BSMR_HIP(hipMemsetAsync(L.sweepDone.data(), 0, static_cast<size_t>(XCD_BUCKETS) * L.sweepSteps * 4, s));
-    }
     a.tilePanel = p.denseItems.data();
     a.tileIds = L.tileIds.data();
     a.denseCols = p.denseCols.data();
@@ -1655,7 +1587,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, sweep, L.dynBatches && !sweep)
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, L.dynBatches)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
@@ -1670,7 +1602,7 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
 #undef BSMR_RB2
 #undef BSMR_RB
     // the workgroup's LDS: 160 / 80 KiB (the image, the staged-output slots, the batch counter)
-    const u32 grid = sweep ? XCD_BUCKETS * L.sweepW : a.pairs ? L.nItems / 2 : L.nItems;
+    const u32 grid = a.pairs ? L.nItems / 2 : L.nItems;
     hipLaunchKernelGGL(fn, dim3(grid, nb), dim3(L.NT),
                        (L.NT == 1024 ? 160 : 80) * 1024, s, a);
     BSMR_HIP(hipGetLastError());
@@ -1709,20 +1641,22 @@ int launch_panels(SddmmArgs a, hipStream_t s) {
 // in L2, no stores) nor nt staging / early B loads
 bool rb_uses_pairs(const Plan& p, const Plan::RowBlockLayout& L) {
     const bool stageNt = p.stage_nt == 1 || (p.stage_nt == -1 && L.outLds != 0 && p.stage_nt_auto);
-    return !L.sweep && L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= p.pair_min_items &&
+    return L.outRuns && L.outLds && L.rowBytes >= 512 && L.nItems >= p.pair_min_items &&
            L.nTilesKept == 0 && L.nItems % (2 * XCD_BUCKETS) == 0 && !stageNt && p.late_b != 0 &&
            !(p.diag & (8u | 32u | 64u | 128u | 16384u));
 }
 
 // whether bsmr_sddmm runs the dense-sampled launch for (K, dtype) (plan_check.cpp)
 bool sddmm_uses_dense(const Plan& p, u32 K, int dtype) { return use_dense(p, K, dtype); }
+// whether bsmr_sddmm runs the panel-grouped tile launch for (K, dtype) (plan_check.cpp, stats)
+bool sddmm_uses_ptile(const Plan& p, u32 K, int dtype) { return use_ptile(p, K, dtype); }
 
 // the whole plan's row-block layout for (K, dtype), built on first use; *out = null when that
 // (K, dtype) runs the column-major launch
 int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out) {
     *out = nullptr;
     const int slot = rb_slot(p, K, dtype);
-    if (slot < 0) return BSMR_OK;
+    if (slot < 0 || use_ptile(p, K, dtype)) return BSMR_OK;
     std::shared_ptr<const Plan::RowBlockLayout> L;  // the whole plan's: a plan member
     BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
     *out = L.get();
@@ -1754,6 +1688,10 @@ extern "C" int bsmr_sddmm_batch(const bsmr_plan* plan, uint32_t num_batch, const
         const char* A = static_cast<const char*>(dA) + es * b0 * static_cast<size_t>(p.M) * K;
         const char* B = static_cast<const char*>(dB) + es * b0 * static_cast<size_t>(p.N) * K;
         float* P = dP + static_cast<size_t>(b0) * p.nnz;
+        if (use_ptile(p, K, dtype)) {
+            BSMR_CHECK(launch_ptile(p, A, B, K, dtype, P, 3, s, nb));
+            continue;
+        }
         if (use_dense(p, K, dtype)) {
             BSMR_CHECK(launch_dense(p, A, B, K, dtype, P, s, nb));
             continue;
@@ -1889,7 +1827,7 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     for (int i = 0; i < 4; ++i) BSMR_HIP(hipEventCreate(&ev[i]));
     const int slot = rb_slot(p, K, dtype);
     std::shared_ptr<const Plan::RowBlockLayout> L;
-    if (slot >= 0) BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
+    if (slot >= 0 && !use_ptile(p, K, dtype)) BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
     SddmmArgs full = make_args(p, dA, dB, K, dP);
     full.nd = p.nDenseItems;
     full.nslots = p.nSlots;
@@ -1897,8 +1835,9 @@ extern "C" int bsmr_sddmm_profile(const bsmr_plan* plan, const void* dA, const v
     dense.nslots = 0;
     SddmmArgs res = full;
     res.nd = 0;
-    const bool dense_all = use_dense(p, K, dtype);
+    const bool ptile = use_ptile(p, K, dtype), dense_all = !ptile && use_dense(p, K, dtype);
     auto run = [&](u32 mode) -> int {
+        if (ptile) return launch_ptile(p, dA, dB, K, dtype, dP, mode, s);
         if (dense_all) return launch_dense(p, dA, dB, K, dtype, dP, s);  // no dense/residual split
         if (L) return launch_rb(p, *L, dA, dB, dP, dtype, mode, s);
         if (dtype != BSMR_F32) return launch_half(p, dA, dB, K, dtype, dP, mode, s);

@@ -164,7 +164,190 @@ __global__ __launch_bounds__(64) void k_sddmm_half(HalfArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Panel-grouped tile launch (tile-dominated fp16 / bf16 plans, e.g. the 16 x 16 block masks of
+// BASELINE.json C5): the reference's design — every BSMR dense tile on the tensor cores
+// (sddmmKernel.cu:213-351, launched per row panel at 2570-2581) — with the panel's A rows staged
+// ONCE per workgroup instead of once per tile.
+//
+// Item i = {panel q, first tile t0, tiles nt} (<= PtileLayout::tpi tiles of one panel). One
+// 256-thread workgroup per item: the panel's 16 A rows (16 x 2K bytes) go to LDS through
+// registers, chunk c of row r at 16-byte slot 4NK r + (c ^ swz(r)) so the 16 rows of a
+// ds_read_b128 lane group hit 16 distinct bank groups; wave w takes tiles t0 + w, t0 + w + 4, ...
+// Lane (rr, g) = (l & 15, l >> 4) holds B[col rr][32 s + 8 g, +8) of every k-step s in registers
+// (NK = K / 32 16-byte loads straight from L2, the next tile's in flight while this one runs its
+// NK `v_mfma_f32_16x16x32_{f16,bf16}`), reads A[row rr][32 s + 8 g, +8) from LDS and scatters
+// D[4 g + r][rr] to P[blockValues[256 t + 16 (4 g + r) + rr]] (NULLV = no stored entry: rows past
+// the last reordered row, sentinel columns, empty slots). Ingest per tile: 16 B rows; per item:
+// 16 A rows — against 16 + 16 rows per tile when each tile loads its own A (k_sddmm_half) and
+// 128 + 128 rows per 128 x 128 tile of the dense-sampled launch.
+// Workgroups past the items run 4 residual slots each (residual_h, one per wave; the column-major
+// slots' XCD deal holds because the item count is a multiple of 8).
+struct PtileArgs {
+    HalfArgs h;
+    const uint4* items;  // {panel, first tile, tiles, 0} in launch order; tiles = 0: padding
+    u32 nItems;          // item slots (a multiple of 8)
+    const u32* rows;     // reordered rows
+    u32 R;
+};
+
+template <u32 NK>
+__device__ __forceinline__ u32 ptile_slot(u32 r, u32 c) {
+    // 4 NK 16-byte chunks per row; rows of >= 16 chunks XOR the low 4 bits with the row
+    return 4 * NK * r + (c ^ (NK >= 4 ? (r & 15) : (r & 7)));
+}
+
+template <bool BF16, u32 NK>
+__global__ __launch_bounds__(256) void k_sddmm_ptile(PtileArgs a) {
+    static_assert(NK == 2 || NK == 4 || NK == 8 || NK == 16, "K / 32 in {2, 4, 8, 16}");
+    __shared__ __attribute__((aligned(16))) s16x8 sa[16 * 4 * NK];
+    if (blockIdx.y) {
+        a.h.A += blockIdx.y * a.h.bA;
+        a.h.B += blockIdx.y * a.h.bB;
+        a.h.P += blockIdx.y * a.h.bP;
+    }
+    const u32 b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const u32 w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (b >= a.nItems) {  // residual slots, one per wave
+        const u32 s = (b - a.nItems) * 4 + w;
+        if (s < a.h.nslots) {
+            const uint2 sl = a.h.slots[s];
+            if (sl.x < sl.y) residual_h<BF16>(a.h, sl);
+        }
+        return;
+    }
+    const uint4 it = a.items[b];
+    const u32 q = it.x, t0 = it.y, nt = it.z;
+    if (nt == 0) return;  // uniform: padding slot
+    const u32 K = 32 * NK;
+    const u32 rr = lane & 15, g = lane >> 4;
+    const size_t rowB = static_cast<size_t>(K) * 2;
+    const char* const Ab = reinterpret_cast<const char*>(a.h.A);
+    const char* const Bb = reinterpret_cast<const char*>(a.h.B);
+    // the wave's tile j: B fragments (one 16-byte load per k-step) and its four output positions
+    auto load_tile = [&](const u32 j, s16x8 (&bf)[NK], u32 (&idx)[4]) {
+        const u32 tile = t0 + j;
+        const u32 c = a.h.denseCols[tile * 16 + rr];
+        const char* bp = Bb + static_cast<size_t>(c < a.h.N ? c : 0) * rowB + 16 * g;
+#pragma unroll
+        for (u32 s = 0; s < NK; ++s) bf[s] = *reinterpret_cast<const s16x8*>(bp + 64 * s);
+        const u32* bv = a.h.blockValues + static_cast<size_t>(tile) * 256 + 64 * g + rr;
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) idx[r] = bv[16 * r];
+    };
+    s16x8 b0[NK], b1[NK];
+    u32 i0[4], i1[4];
+    if (w < nt) load_tile(w, b0, i0);
+    // the panel's A rows: 64 NK chunks of 16 bytes, thread tid takes chunks tid, tid + 256, ...
+    constexpr u32 CPR = 4 * NK, NCH = 16 * CPR, PER = (NCH + 255) / 256;
+    s16x8 av[PER];
+    u32 af[PER];
+#pragma unroll
+    for (u32 i = 0; i < PER; ++i) {
+        const u32 f = tid + 256 * i;
+        af[i] = f;
+        if (NCH % 256 == 0 || f < NCH) {
+            const u32 r = f / CPR, c = f % CPR, x = 16 * q + r;
+            const u32 row = x < a.R ? a.rows[x] : a.rows[0];
+            av[i] = *reinterpret_cast<const s16x8*>(Ab + static_cast<size_t>(row) * rowB + 16 * c);
+        }
+    }
+#pragma unroll
+    for (u32 i = 0; i < PER; ++i)
+        if (NCH % 256 == 0 || af[i] < NCH) sa[ptile_slot<NK>(af[i] / CPR, af[i] % CPR)] = av[i];
+    __syncthreads();
+    // tile j from (bf, idx): NK MFMAs, A fragments from LDS, scatter
+    auto run_tile = [&](const s16x8 (&bf)[NK], const u32 (&idx)[4]) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (u32 s = 0; s < NK; ++s) acc = mfma32<BF16>(sa[ptile_slot<NK>(rr, 4 * s + g)], bf[s], acc);
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r)
+            if (idx[r] != NULLV) a.h.P[idx[r]] = acc[r];
+    };
+    // two register sets alternate so the next tile's loads are in flight under this tile's MFMAs
+    for (u32 j = w; j < nt; j += 8) {
+        if (j + 4 < nt) load_tile(j + 4, b1, i1);
+        run_tile(b0, i0);
+        if (j + 4 >= nt) break;
+        if (j + 8 < nt) load_tile(j + 8, b0, i0);
+        run_tile(b1, i1);
+    }
+}
+
 }  // namespace
+
+// Items of the panel-grouped tile launch (built on first use, per tiles-per-item): every panel's
+// tiles cut into runs of <= tpi; the list is dealt as contiguous eighths per XCD (slot b on XCD
+// b % 8 takes list position (b % 8) per + b / 8), so an XCD's panels are neighbours.
+int Plan::build_ptile_layout(u32 tpi) const {
+    PtileLayout& L = ptile;
+    std::vector<uint4> list;
+    for (u32 q = 0; q < P; ++q) {
+        const u32 a = h_blockOffsets[q], e = h_blockOffsets[q + 1];
+        for (u32 t = a; t < e; t += tpi) list.push_back(make_uint4(q, t, std::min(tpi, e - t), 0));
+    }
+    const u32 n = static_cast<u32>(list.size());
+    const u32 per = (n + XCD_BUCKETS - 1) / XCD_BUCKETS;
+    std::vector<uint4> slots(static_cast<size_t>(per) * XCD_BUCKETS, make_uint4(0, 0, 0, 0));
+    for (u32 b = 0; b < slots.size(); ++b) {
+        const u32 pos = (b % XCD_BUCKETS) * per + b / XCD_BUCKETS;
+        if (pos < n) slots[b] = list[pos];
+    }
+    BSMR_CHECK(L.items.upload(slots.data(), std::max<size_t>(slots.size(), 1), stream));
+    BSMR_HIP(hipStreamSynchronize(stream));  // `slots` is pageable host memory
+    L.nItems = static_cast<u32>(slots.size());
+    L.nListed = n;
+    L.tpi = tpi;
+    L.built = true;
+    return BSMR_OK;
+}
+
+// tile-dominated fp16/bf16 plans, K in {64, 128, 256, 512}: the panel-grouped tile launch (mode: 1
+// tiles, 2 residual slots, 3 both)
+int launch_ptile(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,
+                 u32 mode, hipStream_t s, u32 nb) {
+    const u32 NK = K / 32;
+    if (K % 32 != 0 || (NK != 2 && NK != 4 && NK != 8 && NK != 16)) {
+        set_error("bsmr_sddmm: the panel-tile launch needs K in {64, 128, 256, 512}");
+        return BSMR_ERR_UNSUPPORTED;
+    }
+    {
+        std::lock_guard<std::mutex> g(p.layout_mu);
+        if (!p.ptile.built || p.ptile.tpi != p.ptile_tpi) BSMR_CHECK(p.build_ptile_layout(p.ptile_tpi));
+    }
+    PtileArgs a{};
+    a.h.A = static_cast<const uint16_t*>(dA);
+    a.h.B = static_cast<const uint16_t*>(dB);
+    a.h.P = dP;
+    a.h.nslots = (mode & 2) ? p.nSlots : 0;
+    a.h.denseCols = p.denseCols.data();
+    a.h.blockValues = p.blockValues.data();
+    a.h.slots = p.cmSlots.data();
+    a.h.cmRow = p.cmRow.data();
+    a.h.cmCol = p.cmCol.data();
+    a.h.cmOut = p.cmOut.data();
+    a.h.N = p.N;
+    a.h.K = K;
+    a.h.bA = static_cast<unsigned long long>(p.M) * K;
+    a.h.bB = static_cast<unsigned long long>(p.N) * K;
+    a.h.bP = p.nnz;
+    a.items = p.ptile.items.data();
+    a.nItems = (mode & 1) ? p.ptile.nItems : 0;
+    a.rows = p.rows.data();
+    a.R = p.R;
+    const u32 grid = a.nItems + (a.h.nslots + 3) / 4;
+    if (grid == 0) return BSMR_OK;
+    const bool bf = dtype == BSMR_BF16;
+    const dim3 gd(grid, nb), bd(256);
+    void (*fn)(PtileArgs) = NK == 2   ? (bf ? k_sddmm_ptile<true, 2> : k_sddmm_ptile<false, 2>)
+                            : NK == 4 ? (bf ? k_sddmm_ptile<true, 4> : k_sddmm_ptile<false, 4>)
+                            : NK == 8 ? (bf ? k_sddmm_ptile<true, 8> : k_sddmm_ptile<false, 8>)
+                                      : (bf ? k_sddmm_ptile<true, 16> : k_sddmm_ptile<false, 16>);
+    hipLaunchKernelGGL(fn, gd, bd, 0, s, a);
+    BSMR_HIP(hipGetLastError());
+    return BSMR_OK;
+}
 
 // dtype: BSMR_F16 or BSMR_BF16; K a positive multiple of 32. mode: 1 dense, 2 residual, 3 both
 int launch_half(const Plan& p, const void* dA, const void* dB, u32 K, int dtype, float* dP,

@@ -304,7 +304,6 @@ def test_panel_shards_rowblock_kernel(K, dtype, world):
     ({"BSMR_L2_RANGE_KB": "64"}, 128, 0),      # m > 1 column ranges per XCD, several rounds
     ({"BSMR_L2_RANGE_KB": "64", "BSMR_TILE_MIN_F32": "0"}, 64, 0),
     ({"BSMR_L2_RANGE_KB": "64"}, 256, 1),
-    ({"BSMR_PIECE_ORDER": "1"}, 128, 0),
     ({"BSMR_PIECE_WEIGHT": "0"}, 128, 0),     # item cut by entries + tiles only
     ({"BSMR_PIECE_WEIGHT": "16"}, 256, 1),    # pieces dominate the item cost
     ({"BSMR_SHARD_PIECE_WEIGHT": "1"}, 128, 0),   # shard cuts (checked below) by entries mostly
@@ -368,11 +367,7 @@ def wide_case():
     ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "8192"}, 128, 0),  # the same, set explicitly
     ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "4096"}, 128, 0),  # the round-3 staged rule
     ({}, 128, 0),                                                  # unstaged (P < 8 MiB)
-    # range sweep (k_sddmm_rb_sweep; opt-in, BSMR_SWEEP=1): default knobs, no slack and no task
-    # above the mean, small ranges in bf16
-    ({"BSMR_OUT_STAGED": "1", "BSMR_SWEEP": "1"}, 128, 0),
-    ({"BSMR_OUT_STAGED": "1", "BSMR_SWEEP": "1", "BSMR_SWEEP_SLACK": "0", "BSMR_SWEEP_SPLIT": "1"}, 128, 0),
-    ({"BSMR_OUT_STAGED": "1", "BSMR_SWEEP": "1", "BSMR_SWEEP_RANGE_KB": "512", "BSMR_SWEEP_SLACK": "3"}, 256, 2),
+    ({"BSMR_OUT_STAGED": "1", "BSMR_L2_RANGE_KB": "512"}, 256, 2),  # small ranges in bf16
 ])
 def test_staged_default_column_ranges_wide(env, K, dtype):
     """The staged 512-byte-row default (8 MiB XCD column ranges, plan.hip build_rowblock_layout)
@@ -392,73 +387,9 @@ def test_staged_default_column_ranges_wide(env, K, dtype):
     s = plan.stats()  # 512-byte rows: layout slot 2 (fp32 K = 128, half K = 256)
     rb = s["rb_rows"][2]
     assert rb > 0 and s["rb_items"][2] > (s["num_reordered_rows"] + rb - 1) // rb
-    # the range sweep runs exactly where it is asked for: staged output, not switched off, over
-    # reordered rows with no kept MFMA tile (plan.hip build_rowblock_layout, sweepWanted)
-    applies = not (s["rb_orig_rows"] & 4) and s["rb_tiles"][2] == 0
-    asked = env.get("BSMR_OUT_STAGED") == "1" and env.get("BSMR_SWEEP") == "1"
-    assert bool(s["rb_sweep"] & 4) == (asked and applies)
-    if dtype == 0 and asked:
-        assert s["rb_sweep"] & 4  # fp32 keeps no tile on this pattern: the sweep runs
     shards = [plan.shard(K, r, 2, dtype) for r in range(2)]
     Ps = run_sddmm(plan, A, B, K, len(ci), panels=shards, dtype=dtype)
     assert np.isfinite(Ps).all() and O.check_data(ref, Ps) == 0
-
-
-@pytest.mark.parametrize("K,dtype", [(128, 0), (64, 1), (512, 0)])
-def test_range_sweep_matches_plain_staged(K, dtype):
-    """The range sweep regroups the row-block items into per-workgroup task lists (k_sddmm_rb_sweep):
-    every entry is written (P is NaN-initialised), P passes checkData against the oracle, and it
-    agrees with the plain staged launch to fp32 rounding. Not bit for bit: the chunk order a lane
-    sums in rotates with the row-group that runs the entry's piece (sddmm.hip rot[]), and the
-    sweep cuts pieces at its own column ranges."""
-    M, N, rp, ci = wide_case()
-    A = make_data(M * K)
-    B = make_data(N * K)
-    outs = []
-    for sweep in ("1", "0"):
-        plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock",
-                    tuning=tuning_from_env({"BSMR_OUT_STAGED": "1", "BSMR_SWEEP": sweep,
-                                            "BSMR_SWEEP_RANGE_KB": "1024"}))
-        outs.append(run_sddmm(plan, A, B, K, len(ci), dtype=dtype))
-        slot = {128: 0, 256: 1, 512: 2, 1024: 3, 2048: 4}[K * (4 if dtype == 0 else 2)]
-        on = bool(plan.stats()["rb_sweep"] >> slot & 1)
-        # off when switched off; on for C4's 512-byte fp32 rows (other row sizes take it where
-        # their launch geometry allows: 1024-thread workgroups, >= 2 ranges, a run table)
-        assert not on if sweep == "0" else (on or K * 4 != 512 or dtype != 0)
-    if dtype:
-        A, B = half_values(A, dtype), half_values(B, dtype)
-    ref = O.sddmm_cpu(O.CSR.from_arrays(M, N, rp, ci), K, A, B)
-    for P in outs:
-        assert np.isfinite(P).all() and O.check_data(ref, P) == 0
-    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-5, atol=1e-5 * np.abs(outs[1]).max())
-
-
-def test_range_sweep_layout_batched():
-    """A range-sweep layout launched for several batches (bsmr_sddmm_batch): the sweep's per-XCD
-    step counters serve one batch, so batched launches run the layout's items on the plain
-    row-block kernel; every batch passes checkData."""
-    torch = torch_cuda()
-    M, N, rp, ci = wide_case()
-    K, nb = 128, 2
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, layout="rowblock",
-                tuning=tuning_from_env({"BSMR_OUT_STAGED": "1", "BSMR_SWEEP": "1",
-                                        "BSMR_SWEEP_RANGE_KB": "1024"}))
-    A = make_data(nb * M * K)
-    B = make_data(nb * N * K)[::-1].copy()
-    dA = torch.from_numpy(A).cuda()
-    dB = torch.from_numpy(B).cuda()
-    nnz = len(ci)
-    dP = torch.full((nb * nnz,), float("nan"), dtype=torch.float32, device="cuda")
-    plan.sddmm_batch(nb, dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(),
-                     stream=torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    assert plan.stats()["rb_sweep"] >> 2 & 1
-    P = dP.cpu().numpy()
-    c = O.CSR.from_arrays(M, N, rp, ci)
-    for b in range(nb):
-        ref = O.sddmm_cpu(c, K, A[b * M * K:(b + 1) * M * K], B[b * N * K:(b + 1) * N * K])
-        assert np.isfinite(P[b * nnz:(b + 1) * nnz]).all()
-        assert O.check_data(ref, P[b * nnz:(b + 1) * nnz]) == 0, b
 
 
 def test_values_independent_of_layout_permutation():

@@ -127,13 +127,14 @@ def test_plan_and_launch_layout_pass(name, capfd):
 def test_pairs_with_padding_inside_a_pair():
     """k_sddmm_rb_pair runs list positions 2j and 2j + 1 of an XCD; a list of odd length ends in a
     pair whose second item is padding (never a padding first item: padding is a suffix). Patterns
-    whose lists have odd lengths (one item per segment, or unsplit banded row blocks dealt by the
-    slot model) must compute every entry (pairs untested)."""
+    whose lists have odd lengths (unsplit banded row blocks dealt by the slot model, cost-cut
+    chunks) must compute every entry (pairs untested)."""
     found_odd = 0
-    cases = [(synth.random_rows(1200, 30000, 180, seed=31, zipf=1.05), {"seg_items": 1}),
-             (synth.random_rows(1500, 40000, 150, seed=32, zipf=1.1), {"seg_items": 1}),
-             (synth.banded_fem_like(30000, 22, 5, band=48), {}),
-             (synth.random_rows(1200, 30000, 180, seed=33, zipf=1.05), {})]
+    cases = [(synth.banded_fem_like(30000, 22, 5, band=48), {}),
+             (synth.banded_fem_like(21000, 18, 6, band=40), {}),
+             (synth.random_rows(1200, 30000, 180, seed=33, zipf=1.05), {}),
+             (synth.random_rows(1500, 40000, 150, seed=32, zipf=1.1), {}),
+             (synth.random_rows(1100, 25000, 170, seed=34, zipf=1.05), {"item_cap": 1.0})]
     for (M, N, rp, ci), extra in cases:
         plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,
                     tuning=dict({"out_staged": 1, "pair_min_items": 16}, **extra))
