@@ -11,7 +11,8 @@ Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N,
 `bench.py --gpus N`, which starts that launcher as a child process; a WORLD_SIZE other than
 --gpus is an error, so the line's n_gpus is always --gpus): S sharded by
 row panels (bsmr/dist.py); B is broadcast once from rank 0 over RCCL (xGMI), each
-rank holds only its rows of A, and after timing P is sum-reduced to rank 0 and checked against the
+rank holds only its rows of A, and after timing P is gathered to rank 0 (bit-exact: each rank's
+outputs compacted in plan order, or its contiguous CSR segment) and checked against the
 product's host SDDMM (checkData rule). C2 (default) is weak scaling: the global pattern is N
 copies of the nips-like pattern stacked vertically, copy b with its columns relabelled by a random
 permutation (synth.stack_copies), so per-GPU work stays one C2; C3/C4/C5 are strong scaling of the
@@ -113,21 +114,36 @@ def workload(args):
 
 
 def host_threads():
-    """Host threads for the CPU legs: OMP_NUM_THREADS (the box's CPU share) or all cores, capped
-    at 16 — a one-GPU box's share; os.cpu_count() there is the whole machine's, and a box has
-    been seen exporting OMP_NUM_THREADS=256, which oversubscribes a shared host."""
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    return max(1, min(16, n))
+    """Host threads for the CPU legs (OMP_NUM_THREADS = nproc): OMP_NUM_THREADS
+    when the environment sets it — a GPU box exports its CPU share there (16 per GPU) — else
+    every CPU this process may run on (its affinity mask), never more than that mask."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return max(1, min(n, aff))
 
 
-def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200):
+def host_cpu_info(threads):
+    """What the CPU leg ran on (core count, binding, CPU model)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"threads": threads, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+            "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"),
+            "OMP_PLACES": os.environ.get("OMP_PLACES"), "model": cpu_model()}
+
+
+def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200, max_budget_s=75.0):
     """Time fn() until the last `window` runs agree within `tol` (max / min - 1), or the time
     budget ends (at least `window` runs either way). Returns (median of the last window in s,
     every run's seconds, whether the window converged). The first runs of a host loop on a fresh
     box fall steadily (page faults, frequency ramp: 3.1 -> 0.9 ms over 50 runs of C1 in round 3),
-    so a median over all runs mixes the warm-up drift into the figure."""
+    so a median over all runs mixes the warm-up drift into the figure. Long runs (C4 x1: ~3 s at
+    16 threads) get room for 20 of them: budget max(budget_s, 20 x the first run), at most
+    max_budget_s."""
     times = []
-    t_end = time.perf_counter() + budget_s
+    t0 = time.perf_counter()
+    fn()
+    times.append(time.perf_counter() - t0)
+    t_end = t0 + min(max_budget_s, max(budget_s, 20.0 * times[0]))
     while True:
         t0 = time.perf_counter()
         fn()
@@ -228,10 +244,12 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
         "kind": "port",
         "sample": f"{full} (nnz={nnz_s}, K={K}), median of the last 5 of {len(times)} runs "
                   f"({'within 5 %' if ok else 'time budget reached before 5 runs agreed within 5 %'}), "
-                  f"OpenMP over rows (oracle/oracle.cpp orc_sddmm_cpu_rows); cpu: {model}",
+                  f"OpenMP over rows (oracle/oracle.cpp orc_sddmm_cpu_rows, OMP_PROC_BIND="
+                  f"{os.environ.get('OMP_PROC_BIND')}); cpu: {model}",
         "ms": round(med * 1e3, 3),
         "steady": ok,
         "runs_ms": [round(t * 1e3, 3) for t in times],
+        "host": host_cpu_info(threads),
         "checkData_errors_vs_gpu": nerr,
     }
 
@@ -553,6 +571,10 @@ def self_launch(args):
 
 
 def main():
+    # the CPU legs run OpenMP threads bound close (set before any OpenMP runtime
+    # loads: torch's and the oracle's read them at start-up); a caller's own setting stays
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PLACES", "cores")
     args = parse()
     from bsmr import dist as D
 
@@ -670,11 +692,12 @@ def main_c1(args):
                    "M": M, "N": N, "nnz": nnz, "K": K,
                    "parallelism": f"host: {threads} threads (bsmr_sddmm_cpu, rows split into "
                                   "equal-entry ranges)"},
-        "cpu": {"cores": threads, "model": cpu_model(), "kind": "product host SDDMM "
+        "cpu": {"cores": threads, "model": cpu_model(), "host": host_cpu_info(threads),
+                "kind": "product host SDDMM "
                 "(csrc/host_check.cpp, host.cpp:45-76 loop order, no FMA contraction)",
                 "runs_ms": [round(t * 1e3, 4) for t in times], "steady": steady,
-                "rule": "runs until the last 5 agree within 5 % (20 s budget); value = median of "
-                        "the last 5"},
+                "rule": "runs until the last 5 agree within 5 % (budget max(20 s, 20 runs)); "
+                        "value = median of the last 5"},
         "checkData_errors_cpu_vs_gpu": nerr,
         "gpu_same_workload": {"value": round(flops / (gpu_ms * 1e-3) / 1e9, 2),
                               "ms_per_step": round(gpu_ms, 5), "steps": args.steps,
@@ -962,7 +985,7 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
     """Row-panel shards of ONE global BSMR plan (the reference layout): rank 0
     clusters and broadcasts the row stage over RCCL, every rank rebuilds the column stage, cuts the
     same contiguous panel ranges, holds only its panels' A rows and runs bsmr_sddmm_panels_local;
-    B broadcast once; P sum-reduced to rank 0. time_whole: rank 0 also times the unsharded
+    B broadcast once; P gathered to rank 0 compacted in plan order (bit-exact). time_whole: rank 0 also times the unsharded
     whole-plan launch (the N = 1 point of the same plan) before the shards run. Returns the
     report dict on rank 0 (with the gathered P under "_P"), None elsewhere."""
     import numpy as np
@@ -1012,9 +1035,6 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
 
     def use(c):  # this rank's panels of cuts c and their A rows on the device
         cur["p0"], cur["p1"] = c[rank], c[rank + 1]
-        # outputs of the previous cut's panels would survive in this rank's P and be summed
-        # twice by the gather: every cut starts from a zeroed P
-        dP.zero_()
         A_local = D.shard_a_rows(A, K, rows, cur["p0"], cur["p1"])
         cur["dA"] = torch.from_numpy(A_local.reshape(-1)).to(dev).to(tdt)
         if cur["dA"].numel() == 0:
@@ -1050,13 +1070,16 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
     ms_mine = _timed_steps(step, args.steps, args.warmup, stream, not args.no_graph,
                            cur["p1"] > cur["p0"])
     ms_all = D.all_values(ms_mine, dev)
-    lens = np.diff(np.asarray(rp, dtype=np.int64))
-    mine = int(lens[rows[16 * p0:min(16 * p1, len(rows))]].sum())
-    entries_all = D.all_values(mine, dev)
+    # every rank's output positions in plan order, from the plan every rank holds (nothing sent)
+    pos_all = [D.shard_positions(rp, rows, cuts[r], cuts[r + 1]) for r in range(world)]
+    counts = [len(x) for x in pos_all]
+    mine = counts[rank]
+    entries_all = [float(c) for c in counts]
     panels_all = D.all_values(p1 - p0, dev)
     torch.cuda.synchronize()
     tg = time.perf_counter()
-    P = D.gather_p(dP, 0)  # sum-reduce: each output written by exactly one rank
+    # each rank sends its outputs compacted in plan order, rank 0 scatters them (bit-exact)
+    P = D.gather_compact(dP, pos_all[rank], counts, nnz, pos_all if rank == 0 else None, 0)
     gather_ms = (time.perf_counter() - tg) * 1e3
     st_after = plan.stats()
     if rank != 0:
@@ -1067,7 +1090,8 @@ def shard_global(args, rank, world, wl, dev, time_whole=False):
         "split": "global",
         "parallelism": (f"row-panel shards x{world} of one global BSMR plan (rank 0 clusters, row "
                         "stage broadcast over RCCL, column stage rebuilt per rank), A rows local "
-                        "to their shard, B broadcast once (RCCL), P sum-reduced to rank 0"),
+                        "to their shard, B broadcast once (RCCL), P gathered to rank 0 compacted "
+                        "in plan order (bit-exact)"),
         "ms_per_step": round(ms, 5),
         "value": round(2.0 * nnz * K / (ms * 1e-3) / 1e9, 2),
         "num_clusters": st["num_clusters"], "num_row_panels": st["num_row_panels"],

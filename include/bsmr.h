@@ -32,7 +32,7 @@ extern "C" {
                               bsmr_tuning.pair_min_items, stats rb_pairs;
                               11: bsmr_tuning.batches, stats rb_batches;
                               12: bsmr_tuning.ptile / ptile_tpi (panel-grouped fp16/bf16 tile
-                              launch), stats ptile_items; removed the dropped experiments'
+                              launch), stats ptile_items, bsmr_cost_cuts; removed the dropped experiments'
                               knobs piece_order, seg_items, sweep* and stats rb_sweep */
 
 typedef enum {
@@ -355,6 +355,14 @@ int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int dtype, int 
  * cuts[world]=P. */
 int bsmr_shard_cuts(const uint32_t* blockOffsets, const uint32_t* sparseValueOffsets, uint32_t P,
                     uint32_t K, int world, uint32_t* cuts);
+/* Host-only form of the row-block cuts behind bsmr_plan_shard_dtype / bsmr_plan_shard_rebalance
+ * (no plan, no device): nblocks blocks of panels_per_block panels (the last may be short; P panels
+ * in all) with model costs block_cost[b]; cuts[0..world] at the block boundary nearest each equal
+ * share of the cumulative cost. With prev_cuts and shard_ms (both or neither): each block's cost
+ * scaled by its previous shard's measured / predicted time first (unmeasured shards keep the mean
+ * factor). Deterministic in its inputs, so every rank derives the same cuts. */
+int bsmr_cost_cuts(const double* block_cost, uint32_t nblocks, uint32_t panels_per_block, uint32_t P,
+                   int world, const uint32_t* prev_cuts, const float* shard_ms, uint32_t* cuts);
 int bsmr_sddmm_panels(const bsmr_plan* plan, const void* dA, const void* dB, uint32_t K,
                       int dtype, float* dP, uint32_t p0, uint32_t p1, void* stream);
 

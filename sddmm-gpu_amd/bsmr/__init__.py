@@ -138,7 +138,7 @@ EXPORTS = [
     "bsmr_sddmm_panels_local",
     "bsmr_plan_export_rows", "bsmr_plan_import_rows",
     "bsmr_sddmm_profile", "bsmr_sddmm_cpu", "bsmr_check_one", "bsmr_check_data",
-    "bsmr_plan_check", "bsmr_check_rphm_arrays",
+    "bsmr_plan_check", "bsmr_check_rphm_arrays", "bsmr_cost_cuts",
 ]
 
 _lib = None
@@ -197,6 +197,7 @@ def lib():
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.bsmr_shard_cuts.argtypes = [_u32p, _u32p, C.c_uint32, C.c_uint32, C.c_int, _u32p]
     L.bsmr_plan_shard_rebalance.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, _u32p, _f32p, _u32p]
+    L.bsmr_cost_cuts.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, vp, vp, _u32p]
     L.bsmr_sddmm_panels.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
                                     C.c_uint32, vp]
     L.bsmr_sddmm_panels_local.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, vp, C.c_uint32,
@@ -493,6 +494,21 @@ def shard_cuts(block_offsets, sparse_value_offsets, K, world):
     cuts = np.zeros(world + 1, np.uint32)
     _check(lib().bsmr_shard_cuts(bo, so, P, K, world, cuts), "bsmr_shard_cuts")
     return cuts
+
+
+def cost_cuts(block_cost, panels_per_block, P, world, prev_cuts=None, shard_ms=None):
+    """bsmr_cost_cuts: row-block cuts of P panels by block costs (host only), optionally re-balanced
+    by the times shard_ms[r] measured on prev_cuts (bsmr_plan_shard_rebalance's rule)."""
+    bc = np.ascontiguousarray(block_cost, np.float64)
+    cuts = np.zeros(world + 1, np.uint32)
+    pc = None if prev_cuts is None else np.ascontiguousarray(prev_cuts, np.uint32)
+    ms = None if shard_ms is None else np.ascontiguousarray(shard_ms, np.float32)
+    if (pc is None) != (ms is None) or (pc is not None and (len(pc) != world + 1 or len(ms) != world)):
+        raise ValueError("cost_cuts: prev_cuts (world + 1) and shard_ms (world) go together")
+    ptr = (lambda a: None if a is None else a.ctypes.data)
+    _check(lib().bsmr_cost_cuts(ptr(bc), len(bc), panels_per_block, P, world, ptr(pc), ptr(ms),
+                                cuts), "bsmr_cost_cuts")
+    return [int(c) for c in cuts]
 
 
 def sddmm_cpu(M, N, rowptr, colidx, K, A, B, threads=0):

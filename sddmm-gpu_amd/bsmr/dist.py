@@ -17,10 +17,11 @@ split built here:
 3. **A partitioned.** A rank uploads only the A rows of its panels, in reordered order
    (``shard_a_rows``), and runs ``bsmr_sddmm_panels_local`` on them.
 4. **B broadcast once** from rank 0 (RCCL), outside the timed region.
-5. **P gathered** to rank 0: the local split gathers each rank's contiguous CSR segment
-   (``gather_segments``, bit-exact); shards of the global plan own scattered rows, so their
-   zero-filled nnz buffers are sum-reduced (``gather_p``: exact up to the sign of a zero output,
-   -0.0 + 0.0 = +0.0).
+5. **P gathered** to rank 0, bit-exact and 1/N of the entries per rank: the local split gathers
+   each rank's contiguous CSR segment (``gather_segments``); a shard of the global plan owns
+   scattered rows, so it sends its outputs compacted in plan order (its reordered rows in turn,
+   each row's CSR segment) and rank 0 scatters them through the positions it derives from the
+   same plan (``shard_positions``, ``gather_compact``) — no arithmetic, so -0.0 stays -0.0.
 
 The timed loop has no collective; the whole-job time is the slowest rank's.
 """
@@ -194,15 +195,50 @@ def shard_a_rows(A, K, reordered_rows, p0, p1):
     return np.ascontiguousarray(A[np.asarray(reordered_rows[16 * p0:q1], dtype=np.int64)])
 
 
-def gather_p(dP, dst=0):
-    """P in CSR order on rank `dst`: every rank wrote only its panels' outputs into a zeroed
-    nnz buffer, so a sum-reduce assembles P (x + 0 = x; exact except that a -0.0 output comes
-    back as +0.0, which checkData cannot see). Returns the host array on dst, None elsewhere."""
+def shard_positions(rowptr, reordered_rows, p0, p1):
+    """CSR positions of the outputs of panels [p0, p1) of a plan, in plan order: the reordered
+    rows 16 p0 .. min(16 p1, R) - 1 in turn, each row's CSR segment [rowptr[r], rowptr[r + 1])
+    (int64). Every rank derives every rank's list from the plan it holds; nothing is sent."""
+    rp = np.asarray(rowptr, dtype=np.int64)
+    rows = np.asarray(reordered_rows[16 * p0:min(16 * p1, len(reordered_rows))], dtype=np.int64)
+    starts = rp[rows]
+    lens = rp[rows + 1] - starts
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    # position j of the list = starts[row of j] + (j - first list index of that row)
+    first = np.cumsum(lens) - lens
+    return np.repeat(starts - first, lens) + np.arange(total, dtype=np.int64)
+
+
+def gather_compact(dP, positions, counts, nnz, all_positions=None, dst=0):
+    """P in CSR order on rank `dst` from row-panel shards of one global plan. This rank wrote its
+    outputs into dP (nnz long; positions = its shard_positions list); it sends them compacted in
+    that order, padded to the longest shard (counts = every rank's list length, the same on every
+    rank). On dst, all_positions[r] is rank r's list: the values are scattered back through it.
+    Bit-exact (no arithmetic, -0.0 included); each rank sends its own entries only. Returns the
+    host array on dst, None elsewhere."""
+    import torch
     import torch.distributed as dist
 
-    c = _comm(dP)
-    dist.reduce(c, dst=dst, op=dist.ReduceOp.SUM)
-    return c.cpu().numpy() if dist.get_rank() == dst else None
+    w, rank = dist.get_world_size(), dist.get_rank()
+    width = max(max(int(c) for c in counts), 1)
+    send = torch.zeros(width, dtype=torch.float32, device=dP.device)
+    n = int(counts[rank])
+    if n:
+        idx = torch.from_numpy(np.ascontiguousarray(positions, np.int64)).to(dP.device)
+        send[:n] = dP.index_select(0, idx)
+    send = _comm(send)
+    bufs = [torch.empty_like(send) for _ in range(w)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst)
+    if rank != dst:
+        return None
+    P = np.zeros(int(nnz), np.float32)
+    for r in range(w):
+        k = int(counts[r])
+        if k:
+            P[np.asarray(all_positions[r], np.int64)] = bufs[r][:k].cpu().numpy()
+    return P
 
 
 def gather_segments(dP_seg, e0, e1, nnz, dst=0):

@@ -526,6 +526,58 @@ void cut_row_blocks(const std::vector<double>& cum, u32 nRB, u32 ppr, u32 P, int
 }
 }  // namespace
 
+extern "C" int bsmr_cost_cuts(const double* block_cost, uint32_t nblocks, uint32_t panels_per_block,
+                              uint32_t P, int world, const uint32_t* prev_cuts,
+                              const float* shard_ms, uint32_t* cuts) {
+    if ((!block_cost && nblocks) || world <= 0 || !cuts || panels_per_block == 0 ||
+        (!prev_cuts) != (!shard_ms)) {
+        set_error("bsmr_cost_cuts: bad arguments");
+        return BSMR_ERR_INVALID;
+    }
+    const u32 nRB = nblocks, ppr = panels_per_block;
+    std::vector<double> scale(nRB, 1.0);
+    double norm = 1.0;
+    if (prev_cuts) {
+        if (prev_cuts[0] != 0 || prev_cuts[world] != P) {
+            set_error("bsmr_plan_shard_rebalance: previous cuts must span [0, P]");
+            return BSMR_ERR_INVALID;
+        }
+        // each block's model cost scaled by its shard's measured / predicted time
+        std::vector<char> measured(nRB, 0);
+        for (int r = 0; r < world; ++r) {
+            if (prev_cuts[r + 1] < prev_cuts[r] || (prev_cuts[r] % ppr && prev_cuts[r] != P)) {
+                set_error("bsmr_plan_shard_rebalance: previous cuts are not row-block boundaries");
+                return BSMR_ERR_INVALID;
+            }
+            const u32 b0 = prev_cuts[r] / ppr, b1 = std::min(nRB, (prev_cuts[r + 1] + ppr - 1) / ppr);
+            double pred = 0.0;
+            for (u32 b = b0; b < b1; ++b) pred += block_cost[b];
+            if (pred <= 0.0 || !(shard_ms[r] > 0.0f) || !std::isfinite(shard_ms[r])) continue;
+            const double f = static_cast<double>(shard_ms[r]) / pred;
+            for (u32 b = b0; b < b1; ++b) {
+                scale[b] = f;
+                measured[b] = 1;
+            }
+        }
+        // normalise the factors of measured blocks to their mean; unmeasured blocks (a shard
+        // whose time is 0 / NaN / inf) take the mean factor, i.e. keep their model cost
+        double fs = 0.0;
+        u32 nf = 0;
+        for (u32 b = 0; b < nRB; ++b)
+            if (measured[b]) {
+                fs += scale[b];
+                ++nf;
+            }
+        norm = nf ? fs / nf : 1.0;
+        for (u32 b = 0; b < nRB; ++b)
+            if (!measured[b]) scale[b] = norm;
+    }
+    std::vector<double> cum(nRB + 1ull, 0.0);
+    for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + block_cost[b] * (scale[b] / norm);
+    cut_row_blocks(cum, nRB, ppr, P, world, cuts);
+    return BSMR_OK;
+}
+
 extern "C" int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int dtype, int world,
                                          const uint32_t* prev_cuts, const float* shard_ms,
                                          uint32_t* cuts) {
@@ -541,45 +593,7 @@ extern "C" int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int 
         set_error("bsmr_plan_shard_rebalance: needs the row-block launch of the reordered plan");
         return BSMR_ERR_UNSUPPORTED;
     }
-    const u32 nRB = L->nRB, ppr = L->RB / 16;
-    if (prev_cuts[0] != 0 || prev_cuts[world] != p.P) {
-        set_error("bsmr_plan_shard_rebalance: previous cuts must span [0, P]");
-        return BSMR_ERR_INVALID;
-    }
-    // each row block's model cost scaled by its shard's measured / predicted time
-    std::vector<double> scale(nRB, 1.0);
-    std::vector<char> measured(nRB, 0);
-    for (int r = 0; r < world; ++r) {
-        if (prev_cuts[r + 1] < prev_cuts[r] || (prev_cuts[r] % ppr && prev_cuts[r] != p.P)) {
-            set_error("bsmr_plan_shard_rebalance: previous cuts are not row-block boundaries");
-            return BSMR_ERR_INVALID;
-        }
-        const u32 b0 = prev_cuts[r] / ppr, b1 = std::min(nRB, (prev_cuts[r + 1] + ppr - 1) / ppr);
-        double pred = 0.0;
-        for (u32 b = b0; b < b1; ++b) pred += L->rbCost[b];
-        if (pred <= 0.0 || !(shard_ms[r] > 0.0f) || !std::isfinite(shard_ms[r])) continue;
-        const double f = static_cast<double>(shard_ms[r]) / pred;
-        for (u32 b = b0; b < b1; ++b) {
-            scale[b] = f;
-            measured[b] = 1;
-        }
-    }
-    // normalise the factors of measured blocks to their mean; unmeasured blocks (a shard whose
-    // time is 0 / NaN / inf) take the mean factor, i.e. keep their model cost
-    double fs = 0.0;
-    u32 nf = 0;
-    for (u32 b = 0; b < nRB; ++b)
-        if (measured[b]) {
-            fs += scale[b];
-            ++nf;
-        }
-    const double norm = nf ? fs / nf : 1.0;
-    for (u32 b = 0; b < nRB; ++b)
-        if (!measured[b]) scale[b] = norm;
-    std::vector<double> cum(nRB + 1ull, 0.0);
-    for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b] * (scale[b] / norm);
-    cut_row_blocks(cum, nRB, ppr, p.P, world, cuts);
-    return BSMR_OK;
+    return bsmr_cost_cuts(L->rbCost.data(), L->nRB, L->RB / 16, p.P, world, prev_cuts, shard_ms, cuts);
 }
 
 extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtype, int rank,
@@ -597,10 +611,8 @@ extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtyp
     const Plan::RowBlockLayout* L = nullptr;
     BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
     if (L && L->nRB > 0 && !L->orig) {  // (original-order row blocks do not map to panels)
-        const u32 nRB = L->nRB, ppr = L->RB / 16;
-        std::vector<double> cum(nRB + 1ull, 0.0);
-        for (u32 b = 0; b < nRB; ++b) cum[b + 1] = cum[b] + L->rbCost[b];
-        cut_row_blocks(cum, nRB, ppr, p.P, world, cuts.data());
+        BSMR_CHECK(bsmr_cost_cuts(L->rbCost.data(), L->nRB, L->RB / 16, p.P, world, nullptr, nullptr,
+                                  cuts.data()));
     } else {
         BSMR_CHECK(bsmr_shard_cuts(p.h_blockOffsets.data(), p.h_sparseValueOffsets.data(), p.P, K,
                                    world, cuts.data()));

@@ -199,7 +199,7 @@ def test_bench_sharded_two_ranks_one_gpu(extra):
 def test_bench_sharded_rccl_one_rank():
     """bench.py's multi-GPU path on RCCL (backend "nccl"), launched by torchrun before any GPU
     call, at world size 1 (--force-sharded: RCCL refuses two ranks on one device): RCCL init, the
-    device-tensor broadcasts (B, row stage, the strong_C4 pattern), the P sum-reduce and the
+    device-tensor broadcasts (B, row stage, the strong_C4 pattern), the compact P gather and the
     segment gather all execute on MI355X; both strong_C4 splits and the C2 line pass checkData."""
     env = dict(os.environ, OMP_NUM_THREADS="8")
     env.pop("BSMR_DIST_BACKEND", None)
