@@ -276,7 +276,7 @@ def rowblock_bounds(st, rby, ms):
     }
 
 
-def mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles):
+def mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles, measured=None):
     """MFMA use of the timed launch (BASELINE.md §3 per-config fields). SURVEY.md §8d's MFMA
     efficiency = 2·nnz_dense·K / (256·2·K·#denseBlocks): stored entries per 16 x 16 output slot of
     the tiles computed on the matrix cores, for the BSMR plan's tiles (the reference's dense
@@ -287,7 +287,10 @@ def mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles):
          "bsmr_plan_tiles": {"tiles": ntiles, "entries": nnz - st["num_residual"],
                              "efficiency": round((nnz - st["num_residual"]) / (256.0 * ntiles), 4)
                              if ntiles else None}}
-    if dtiles:
+    if kern.startswith("k_sddmm_ptile"):
+        r["launch"] = {"kind": "panel-grouped BSMR 16 x 16 tiles, every tile on MFMA", "tiles": ntiles,
+                       "efficiency": r["bsmr_plan_tiles"]["efficiency"]}
+    elif dtiles:
         r["launch"] = {"kind": "dense-sampled 128 x 128 tiles", "tiles": dtiles,
                        "efficiency": round(nnz / (16384.0 * dtiles), 4)}
     elif kern.startswith("k_sddmm_rb"):
@@ -297,10 +300,14 @@ def mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles):
                        "efficiency": round((nnz - st_after["rb_entries"][i]) / (256.0 * kept), 4)
                        if kept else None}
         if no_tiles:
-            r["busy"] = 0.0
             r["busy_note"] = ("no MFMA instruction in this launch: every tile's entries run as "
                               "residual entries on the vector ALUs (fp32 MFMA runs at the vector "
                               "FMA rate on gfx950; half tiles under 128 entries are demoted)")
+    if measured:  # the in-run PMC pass (mfma_busy)
+        r.update(measured)
+    elif no_tiles:
+        r["busy"] = 0.0
+        r["busy_source"] = "by construction (no MFMA instruction; no PMC pass in this run)"
     return r
 
 
@@ -422,6 +429,10 @@ def kernel_name(st, st_after, K, dtype, layout):
     from bsmr import F32
 
     rby = K * (4 if dtype == F32 else 2)
+    if st_after.get("ptile_items"):  # sddmm.hip use_ptile (its item list is built on first use)
+        return (f"k_sddmm_ptile<{'f16' if dtype == 1 else 'bf16'},{K // 32}> (panel-grouped BSMR "
+                f"tiles, every tile on MFMA 16x16x32: a panel's 16 A rows staged in LDS once per "
+                f"item, {st_after['ptile_items']} item slots; residual in column-major slots)"), rby
     tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
     if rby in (128, 256, 512, 1024, 2048) and layout != "colmajor" and not tile_dominated:
         tiles = ("fp32 tiles demoted to residual entries" if dtype == F32
@@ -507,8 +518,10 @@ def pmc_traffic_inrun(args):
     tmp = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
     limit = 600 if args.config == "C4" else 180
     t0 = time.perf_counter()
-    for name, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        cmd = ["timeout", "-s", "KILL", str(limit), rp, "--pmc", ctr, "--kernel-include-regex",
+    # three passes, one counter group each (FETCH_SIZE takes 3 of the 4 TCC counters, WRITE_SIZE
+    # 2; the MFMA group is 6 SQ + 1 GRBM counters)
+    for name, ctr in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"]), ("mfma", MFMA_PMC)):
+        cmd = ["timeout", "-s", "KILL", str(limit), rp, "--pmc"] + ctr + ["--kernel-include-regex",
                "k_sddmm", "--output-format", "csv", "-d", os.path.join(tmp, name), "-o", "run",
                "--", sys.executable, os.path.join(ROOT, "tools", "prof_sddmm.py")] + wl
         r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
@@ -522,15 +535,46 @@ def pmc_traffic_inrun(args):
         full = json.loads(out)["full"]
         fetch = 2.0 * full["FETCH_SIZE"] * 1024.0
         write = full["WRITE_SIZE"] * 1024.0
+        mfma = {c: full.get(c) for c in MFMA_PMC}
     except (subprocess.CalledProcessError, KeyError, ValueError) as e:
         return None, {"status": f"PMC parse failed: {e}"}
     shutil.rmtree(tmp, ignore_errors=True)
     return round(fetch + write), {
         "status": "measured in this run", "fetch_bytes": round(fetch), "write_bytes": round(write),
-        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
-                  "tools/prof_sddmm.py --iters 5, median over the fused launches; FETCH_SIZE "
+        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / the MFMA group (separate passes) "
+                  "over tools/prof_sddmm.py --iters 5, median over the fused launches; FETCH_SIZE "
                   "KiB x 2 (gfx950) + WRITE_SIZE KiB",
+        "mfma_counters": mfma,
         "seconds": round(time.perf_counter() - t0, 1)}
+
+
+# the MFMA counter pass of the in-run PMC (one run: 6 SQ + 1 GRBM counters)
+MFMA_PMC = ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+            "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_INSTS_MFMA",
+            "GRBM_GUI_ACTIVE"]
+
+
+def mfma_busy(counters, nnz, K):
+    """MFMA use of the fused launch from its PMC pass (MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES
+    counts matrix-pipe cycles summed over SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs, so the
+    launch's wall cycles are / 8; 256 CUs x 4 SIMDs; one MFMA MOP = 512 flops)."""
+    busy, grbm = counters.get("SQ_VALU_MFMA_BUSY_CYCLES"), counters.get("GRBM_GUI_ACTIVE")
+    if busy is None or not grbm:
+        return None
+    mops = sum(counters.get(k) or 0.0 for k in MFMA_PMC if k.startswith("SQ_INSTS_VALU_MFMA_MOPS"))
+    wall = grbm / 8.0
+    r = {"busy": round(busy / (wall * 1024.0), 4),
+         "busy_definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the "
+                            "fraction of all SIMD cycles of the launch (under the PMC pass) the "
+                            "matrix pipes were busy",
+         "mfma_instructions": counters.get("SQ_INSTS_MFMA"),
+         "mfma_flops": mops * 512.0,
+         "source": "rocprofv3 --pmc pass in this run (fused launch, median)"}
+    if mops:
+        r["sampled_flops_per_mfma_flop"] = round(2.0 * nnz * K / (mops * 512.0), 4)
+    if counters.get("SQ_BUSY_CU_CYCLES"):
+        r["busy_of_cu_busy_cycles"] = round(busy / (4.0 * counters["SQ_BUSY_CU_CYCLES"]), 4)
+    return r
 
 
 def _free_port():
@@ -877,7 +921,9 @@ def main_single(args):
     }
     if kern.startswith("k_sddmm_rb"):
         out["bounds"] = rowblock_bounds(st_after, rby, ms_per_step)
-    out["mfma"] = mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles)
+    mc = (traffic_src or {}).get("mfma_counters") if isinstance(traffic_src, dict) else None
+    out["mfma"] = mfma_report(st, st_after, nnz, rby, dtiles, kern, no_tiles,
+                              mfma_busy(mc, nnz, K) if mc else None)
     if (no_tiles and not dtiles and not args.no_split and st["num_dense_tiles"] > 0
             and nnz <= 20_000_000):
         out["mfma"]["forced_tiles_split"] = forced_mfma_split(

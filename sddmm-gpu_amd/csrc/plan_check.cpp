@@ -656,6 +656,27 @@ private:
             for (u32 t = it.y; t < it.y + it.z; ++t)
                 if (thit[t]++) return layout_fail(fmt("panel-tile: tile %u in two items", t)), BSMR_OK;
         }
+        // the descriptors the kernel reads: the item's panel rows, tile range and tile columns
+        std::vector<u32> desc;
+        BSMR_CHECK(p_.ptile.desc.download(desc, p_.stream));
+        const u32 ds = Plan::PtileLayout::desc_stride(p_.ptile.tpi);
+        if (desc.size() < static_cast<size_t>(p_.ptile.nItems) * ds)
+            return layout_fail("panel-tile descriptors missing"), BSMR_OK;
+        for (u32 i = 0; i < p_.ptile.nItems; ++i) {
+            const uint4 it = items[i];
+            const u32* d = desc.data() + static_cast<size_t>(i) * ds;
+            if (d[17] != it.z || (it.z && d[16] != it.y))
+                return layout_fail(fmt("panel-tile descriptor %u: tiles [%u, +%u) for item [%u, +%u)", i, d[16], d[17], it.y, it.z)), BSMR_OK;
+            for (u32 r = 0; r < 16 && it.z; ++r) {
+                const u32 x = 16 * it.x + r, want = x < h_.R ? h_.rows[x] : h_.rows[0];
+                if (d[r] != want)
+                    return layout_fail(fmt("panel-tile descriptor %u: row %u is %u, panel row %u", i, r, d[r], want)), BSMR_OK;
+            }
+            for (u32 j = 0; j < it.z; ++j)
+                for (u32 c = 0; c < 16; ++c)
+                    if (d[32 + 16 * j + c] != h_.dcols[static_cast<size_t>(it.y + j) * 16 + c])
+                        return layout_fail(fmt("panel-tile descriptor %u: column %u of tile %u", i, c, it.y + j)), BSMR_OK;
+        }
         for (u32 t = 0; t < nt; ++t)
             if (!thit[t]) return layout_fail(fmt("panel-tile: tile %u in no item", t)), BSMR_OK;
         return cm_layout(ok);
@@ -825,7 +846,8 @@ int run_checks(Checker& c, u32 K, int dtype, int verbose) {
 // Test hook (not in the header; tests/test_gpu_plan_check.py): overwrite element `index` of one
 // plan array (which = a bsmr_array value 0..10) or of the launch layout bsmr_sddmm runs for
 // (K, dtype) (100: row-block entry metadata, 101: row-block piece words {first entry, column |
-// (length - 1) << 22} as 2 u32 per piece, 102: column-major residual output positions), so a
+// (length - 1) << 22} as 2 u32 per piece, 102: column-major residual output positions, 103: the
+// panel-tile launch's item descriptors), so a
 // test can show that bsmr_plan_check catches the corruption. *old receives the previous value.
 extern "C" int bsmr_debug_plan_poke(bsmr_plan* plan, int which, uint64_t index, uint32_t value,
                                     uint32_t K, int dtype, uint32_t* old) {
@@ -864,6 +886,10 @@ extern "C" int bsmr_debug_plan_poke(bsmr_plan* plan, int which, uint64_t index, 
             break;
         }
         case 102: base = p.cmOut.data(); n = p.nres; break;
+        case 103:  // the panel-tile launch's item descriptors (built by the launch or the check)
+            base = p.ptile.built ? p.ptile.desc.data() : nullptr;
+            n = p.ptile.built ? p.ptile.desc.n : 0;
+            break;
         default:
             set_error("bsmr_debug_plan_poke: unknown array");
             return BSMR_ERR_INVALID;

@@ -170,8 +170,9 @@ __global__ __launch_bounds__(64) void k_sddmm_half(HalfArgs a) {
 // (sddmmKernel.cu:213-351, launched per row panel at 2570-2581) — with the panel's A rows staged
 // ONCE per workgroup instead of once per tile.
 //
-// Item i = {panel q, first tile t0, tiles nt} (<= PtileLayout::tpi tiles of one panel). One
-// 256-thread workgroup per item: the panel's 16 A rows (16 x 2K bytes) go to LDS through
+// Item i = {panel q, first tile t0, tiles nt} (<= PtileLayout::tpi tiles of one panel), read from
+// its descriptor (the panel's 16 rows and the tiles' columns inline, so A and B addresses are one
+// load away from the workgroup id). One 256-thread workgroup per item: the panel's 16 A rows (16 x 2K bytes) go to LDS through
 // registers, chunk c of row r at 16-byte slot 4NK r + (c ^ swz(r)) so the 16 rows of a
 // ds_read_b128 lane group hit 16 distinct bank groups; wave w takes tiles t0 + w, t0 + w + 4, ...
 // Lane (rr, g) = (l & 15, l >> 4) holds B[col rr][32 s + 8 g, +8) of every k-step s in registers
@@ -185,10 +186,12 @@ __global__ __launch_bounds__(64) void k_sddmm_half(HalfArgs a) {
 // slots' XCD deal holds because the item count is a multiple of 8).
 struct PtileArgs {
     HalfArgs h;
-    const uint4* items;  // {panel, first tile, tiles, 0} in launch order; tiles = 0: padding
+    const u32* desc;     // per item slot in launch order (PtileLayout::desc); tiles = 0: padding
+    u32 dstride;
     u32 nItems;          // item slots (a multiple of 8)
-    const u32* rows;     // reordered rows
-    u32 R;
+    // BSMR_DIAG & 32: per workgroup {start, A staged (after the barrier), end, xcc << 60 | wave 0's
+    // first tile's MFMAs done} (s_memrealtime, 100 MHz); else null
+    unsigned long long* trace;
 };
 
 template <u32 NK>
@@ -197,9 +200,10 @@ __device__ __forceinline__ u32 ptile_slot(u32 r, u32 c) {
     return 4 * NK * r + (c ^ (NK >= 4 ? (r & 15) : (r & 7)));
 }
 
-template <bool BF16, u32 NK>
-__global__ __launch_bounds__(256) void k_sddmm_ptile(PtileArgs a) {
+template <bool BF16, u32 NK, u32 NW>
+__global__ __launch_bounds__(64 * NW) void k_sddmm_ptile(PtileArgs a) {
     static_assert(NK == 2 || NK == 4 || NK == 8 || NK == 16, "K / 32 in {2, 4, 8, 16}");
+    constexpr u32 NT = 64 * NW;
     __shared__ __attribute__((aligned(16))) s16x8 sa[16 * 4 * NK];
     if (blockIdx.y) {
         a.h.A += blockIdx.y * a.h.bA;
@@ -208,16 +212,18 @@ __global__ __launch_bounds__(256) void k_sddmm_ptile(PtileArgs a) {
     }
     const u32 b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const u32 w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (b >= a.nItems) {  // residual slots, one per wave
+    if (b >= a.nItems) {  // residual slots: 4 per workgroup (the column-major slots' XCD deal)
         const u32 s = (b - a.nItems) * 4 + w;
-        if (s < a.h.nslots) {
+        if (w < 4 && s < a.h.nslots) {
             const uint2 sl = a.h.slots[s];
             if (sl.x < sl.y) residual_h<BF16>(a.h, sl);
         }
         return;
     }
-    const uint4 it = a.items[b];
-    const u32 q = it.x, t0 = it.y, nt = it.z;
+    const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // the item's descriptor: rows d[0..16), first tile d[16], tiles d[17], columns d[32 + 16 j + c]
+    const u32* const d = a.desc + static_cast<size_t>(b) * a.dstride;
+    const u32 t0 = d[16], nt = d[17];
     if (nt == 0) return;  // uniform: padding slot
     const u32 K = 32 * NK;
     const u32 rr = lane & 15, g = lane >> 4;
@@ -225,9 +231,11 @@ __global__ __launch_bounds__(256) void k_sddmm_ptile(PtileArgs a) {
     const char* const Ab = reinterpret_cast<const char*>(a.h.A);
     const char* const Bb = reinterpret_cast<const char*>(a.h.B);
     // the wave's tile j: B fragments (one 16-byte load per k-step) and its four output positions
-    auto load_tile = [&](const u32 j, s16x8 (&bf)[NK], u32 (&idx)[4]) {
+    s16x8 bf[NK];
+    u32 idx[4];
+    auto load_tile = [&](const u32 j) {
         const u32 tile = t0 + j;
-        const u32 c = a.h.denseCols[tile * 16 + rr];
+        const u32 c = d[32 + 16 * j + rr];
         const char* bp = Bb + static_cast<size_t>(c < a.h.N ? c : 0) * rowB + 16 * g;
 #pragma unroll
         for (u32 s = 0; s < NK; ++s) bf[s] = *reinterpret_cast<const s16x8*>(bp + 64 * s);
@@ -235,43 +243,48 @@ __global__ __launch_bounds__(256) void k_sddmm_ptile(PtileArgs a) {
 #pragma unroll
         for (u32 r = 0; r < 4; ++r) idx[r] = bv[16 * r];
     };
-    s16x8 b0[NK], b1[NK];
-    u32 i0[4], i1[4];
-    if (w < nt) load_tile(w, b0, i0);
-    // the panel's A rows: 64 NK chunks of 16 bytes, thread tid takes chunks tid, tid + 256, ...
-    constexpr u32 CPR = 4 * NK, NCH = 16 * CPR, PER = (NCH + 255) / 256;
+    // the first tile's loads go out ahead of the A staging (their latency overlaps it)
+    if (w < nt) load_tile(w);
+    // the panel's A rows: 64 NK chunks of 16 bytes, thread tid takes chunks tid, tid + NT, ...
+    constexpr u32 CPR = 4 * NK, NCH = 16 * CPR, PER = (NCH + NT - 1) / NT;
     s16x8 av[PER];
-    u32 af[PER];
 #pragma unroll
     for (u32 i = 0; i < PER; ++i) {
-        const u32 f = tid + 256 * i;
-        af[i] = f;
-        if (NCH % 256 == 0 || f < NCH) {
-            const u32 r = f / CPR, c = f % CPR, x = 16 * q + r;
-            const u32 row = x < a.R ? a.rows[x] : a.rows[0];
+        const u32 f = tid + NT * i;
+        if (NCH % NT == 0 || f < NCH) {
+            const u32 r = f / CPR, c = f % CPR, row = d[r];
             av[i] = *reinterpret_cast<const s16x8*>(Ab + static_cast<size_t>(row) * rowB + 16 * c);
         }
     }
 #pragma unroll
-    for (u32 i = 0; i < PER; ++i)
-        if (NCH % 256 == 0 || af[i] < NCH) sa[ptile_slot<NK>(af[i] / CPR, af[i] % CPR)] = av[i];
+    for (u32 i = 0; i < PER; ++i) {
+        const u32 f = tid + NT * i;
+        if (NCH % NT == 0 || f < NCH) sa[ptile_slot<NK>(f / CPR, f % CPR)] = av[i];
+    }
     __syncthreads();
-    // tile j from (bf, idx): NK MFMAs, A fragments from LDS, scatter
-    auto run_tile = [&](const s16x8 (&bf)[NK], const u32 (&idx)[4]) {
+    const unsigned long long t_mid = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long t_mfma = 0;
+    // one tile per wave at a time (NK 16-byte B loads in flight per lane): NK MFMAs with A
+    // fragments from LDS, then the scatter
+    for (u32 j = w; j < nt; j += NW) {
+        if (j != w) load_tile(j);
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (u32 s = 0; s < NK; ++s) acc = mfma32<BF16>(sa[ptile_slot<NK>(rr, 4 * s + g)], bf[s], acc);
+        if (a.trace && j == w)  // (reads the result: after the last MFMA)
+            t_mfma = __builtin_amdgcn_s_memrealtime() + (acc[0] != acc[0] ? 1ull : 0ull);
 #pragma unroll
         for (u32 r = 0; r < 4; ++r)
             if (idx[r] != NULLV) a.h.P[idx[r]] = acc[r];
-    };
-    // two register sets alternate so the next tile's loads are in flight under this tile's MFMAs
-    for (u32 j = w; j < nt; j += 8) {
-        if (j + 4 < nt) load_tile(j + 4, b1, i1);
-        run_tile(b0, i0);
-        if (j + 4 >= nt) break;
-        if (j + 8 < nt) load_tile(j + 8, b0, i0);
-        run_tile(b1, i1);
+    }
+    if (a.trace && tid == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        const u32 xcc = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+        unsigned long long* tr = a.trace + 4ull * (blockIdx.y * gridDim.x + blockIdx.x);
+        tr[0] = t_start;
+        tr[1] = t_mid;
+        tr[2] = t_end;
+        tr[3] = (static_cast<unsigned long long>(xcc) << 60) | (t_mfma & ((1ull << 60) - 1));
     }
 }
 
@@ -282,10 +295,15 @@ __global__ __launch_bounds__(256) void k_sddmm_ptile(PtileArgs a) {
 // b % 8 takes list position (b % 8) per + b / 8), so an XCD's panels are neighbours.
 int Plan::build_ptile_layout(u32 tpi) const {
     PtileLayout& L = ptile;
+    // a panel of n tiles: ceil(n / tpi) items of near-equal size (13 at tpi 4: 4, 3, 3, 3)
     std::vector<uint4> list;
     for (u32 q = 0; q < P; ++q) {
-        const u32 a = h_blockOffsets[q], e = h_blockOffsets[q + 1];
-        for (u32 t = a; t < e; t += tpi) list.push_back(make_uint4(q, t, std::min(tpi, e - t), 0));
+        const u32 a = h_blockOffsets[q], n = h_blockOffsets[q + 1] - a, k = (n + tpi - 1) / tpi;
+        for (u32 i = 0; i < k; ++i) {
+            const u32 t0 = a + static_cast<u32>(static_cast<u64>(n) * i / k);
+            const u32 t1 = a + static_cast<u32>(static_cast<u64>(n) * (i + 1) / k);
+            list.push_back(make_uint4(q, t0, t1 - t0, 0));
+        }
     }
     const u32 n = static_cast<u32>(list.size());
     const u32 per = (n + XCD_BUCKETS - 1) / XCD_BUCKETS;
@@ -294,8 +312,29 @@ int Plan::build_ptile_layout(u32 tpi) const {
         const u32 pos = (b % XCD_BUCKETS) * per + b / XCD_BUCKETS;
         if (pos < n) slots[b] = list[pos];
     }
+    // per item slot its descriptor (PtileArgs::desc): the panel's 16 A rows, the first tile and the
+    // tile count, then 16 columns per tile — what the kernel's loads need, one load away
+    std::vector<u32> hrows, hcols;
+    BSMR_CHECK(rows.download(hrows, stream));
+    BSMR_CHECK(denseCols.download(hcols, stream));
+    const u32 ds = PtileLayout::desc_stride(tpi);
+    std::vector<u32> desc(static_cast<size_t>(slots.size()) * ds, 0);
+    for (size_t b = 0; b < slots.size(); ++b) {
+        const uint4 it = slots[b];
+        u32* d = desc.data() + b * ds;
+        if (it.z == 0) continue;
+        for (u32 r = 0; r < 16; ++r) {
+            const u32 x = 16 * it.x + r;
+            d[r] = x < R ? hrows[x] : hrows[0];
+        }
+        d[16] = it.y;
+        d[17] = it.z;
+        for (u32 j = 0; j < it.z; ++j)
+            for (u32 c = 0; c < 16; ++c) d[32 + 16 * j + c] = hcols[(it.y + j) * 16 + c];
+    }
     BSMR_CHECK(L.items.upload(slots.data(), std::max<size_t>(slots.size(), 1), stream));
-    BSMR_HIP(hipStreamSynchronize(stream));  // `slots` is pageable host memory
+    BSMR_CHECK(L.desc.upload(desc.data(), std::max<size_t>(desc.size(), 1), stream));
+    BSMR_HIP(hipStreamSynchronize(stream));  // host vectors are pageable memory
     L.nItems = static_cast<u32>(slots.size());
     L.nListed = n;
     L.tpi = tpi;
@@ -332,19 +371,28 @@ int launch_ptile(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     a.h.bA = static_cast<unsigned long long>(p.M) * K;
     a.h.bB = static_cast<unsigned long long>(p.N) * K;
     a.h.bP = p.nnz;
-    a.items = p.ptile.items.data();
+    a.desc = p.ptile.desc.data();
+    a.dstride = Plan::PtileLayout::desc_stride(p.ptile.tpi);
     a.nItems = (mode & 1) ? p.ptile.nItems : 0;
-    a.rows = p.rows.data();
-    a.R = p.R;
-    const u32 grid = a.nItems + (a.h.nslots + 3) / 4;
-    if (grid == 0) return BSMR_OK;
+    a.trace = nullptr;
+    u32 grid = a.nItems + (a.h.nslots + 3) / 4;
+    if (grid == 0) {
+        if (mode == 3) return BSMR_OK;
+        grid = 1;  // a profiling split with nothing to run (no residual) still dispatches once
+    }
+    if (p.diag & 32) {
+        BSMR_CHECK(p.prepare_trace(static_cast<size_t>(grid) * nb, s));
+        a.trace = p.trace.data();
+    }
     const bool bf = dtype == BSMR_BF16;
-    const dim3 gd(grid, nb), bd(256);
-    void (*fn)(PtileArgs) = NK == 2   ? (bf ? k_sddmm_ptile<true, 2> : k_sddmm_ptile<false, 2>)
-                            : NK == 4 ? (bf ? k_sddmm_ptile<true, 4> : k_sddmm_ptile<false, 4>)
-                            : NK == 8 ? (bf ? k_sddmm_ptile<true, 8> : k_sddmm_ptile<false, 8>)
-                                      : (bf ? k_sddmm_ptile<true, 16> : k_sddmm_ptile<false, 16>);
-    hipLaunchKernelGGL(fn, gd, bd, 0, s, a);
+    const dim3 gd(grid, nb);
+    // waves per workgroup: one per tile of an item up to 8 (items of more tiles loop)
+    const bool w8 = p.ptile.tpi > 4;
+#define BSMR_PT(NKV) (w8 ? (bf ? k_sddmm_ptile<true, NKV, 8> : k_sddmm_ptile<false, NKV, 8>) \
+                         : (bf ? k_sddmm_ptile<true, NKV, 4> : k_sddmm_ptile<false, NKV, 4>))
+    void (*fn)(PtileArgs) = NK == 2 ? BSMR_PT(2) : NK == 4 ? BSMR_PT(4) : NK == 8 ? BSMR_PT(8) : BSMR_PT(16);
+#undef BSMR_PT
+    hipLaunchKernelGGL(fn, gd, dim3(w8 ? 512 : 256), 0, s, a);
     BSMR_HIP(hipGetLastError());
     return BSMR_OK;
 }

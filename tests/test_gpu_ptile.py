@@ -50,7 +50,8 @@ def test_block_mask_every_tile_on_mfma(K, dtype):
 
 @pytest.mark.parametrize("tpi", [1, 3, 8, 64])
 def test_tiles_per_item(tpi):
-    """Items of 1..64 tiles of one panel: waves loop over their tiles (two register sets in turn)."""
+    """Items of 1..64 tiles of one panel: 4 or 8 waves per workgroup, looping over the item's
+    tiles past one per wave."""
     M, N, rp, ci = synth.block_mask(768, 16, 0.2, seed=12)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,
                 tuning={"ptile_tpi": tpi})
@@ -106,3 +107,21 @@ def test_batched_launch():
         ref = _ref(M, N, rp, ci, K, A[b * M * K:(b + 1) * M * K], B[b * N * K:(b + 1) * N * K], 2)
         assert O.check_data(ref, P[b * nnz:(b + 1) * nnz]) == 0
     assert plan.stats()["ptile_items"] > 0
+
+
+@pytest.mark.parametrize("word", ["row", "column", "tiles"])
+def test_corrupted_descriptor_fails_the_layout_check(word):
+    """bsmr_plan_check verifies the descriptors the panel-tile kernel reads (rows, tile range,
+    columns) against the plan; one corrupted word fails with the descriptor's message."""
+    from test_gpu_plan_check import _poke
+    M, N, rp, ci = synth.block_mask(512, 16, 0.15, seed=15)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    assert plan.check(256, 2, verbose=False) == (True, "")  # builds the descriptors
+    items = plan.stats()["ptile_items"]
+    assert items > 0
+    # the first item slot with tiles (slot 0 holds the XCD-0 eighth's first item)
+    idx = {"row": 3, "column": 32 + 5, "tiles": 17}[word]
+    old = _poke(plan, 103, idx, 7, 256, 2)
+    _poke(plan, 103, idx, old ^ 1 if word != "tiles" else old + 1, 256, 2)
+    ok, msg = plan.check(256, 2, verbose=False)
+    assert not ok and "panel-tile descriptor" in msg, msg

@@ -1,0 +1,15 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r06b; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_ptile.py -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest.log; exit 1; }
+Q="--no-cpu-baseline --no-vendor --pmc off --config C5 --steps 100 --warmup 10"
+run() { local name=$1; shift; env "$@" timeout -k 10 300 python3 bench.py $Q $EXTRA > $O/$name.json 2> $O/$name.err || exit 3; }
+for t in 2 3 4 6 8 12; do EXTRA="--mask block" run blk_tpi$t BSMR_PTILE_TPI=$t; done
+EXTRA="--mask block" run blk_off BSMR_PTILE=0
+for K in 128 256; do for t in 4 8; do EXTRA="--mask block --K $K" run blk_K${K}_tpi$t BSMR_PTILE_TPI=$t; done; EXTRA="--mask block --K $K" run blk_K${K}_off BSMR_PTILE=0; done
+EXTRA="--mask uniform" run uni_forced BSMR_PTILE=1 BSMR_PTILE_TPI=4
+python3 - <<'PY'
+import json,glob
+for f in sorted(glob.glob("gpurun_out/r06b/*.json")):
+    d=json.load(open(f)); print(f.split('/')[-1], d.get("value"), d.get("ms_per_step"), (d.get("roofline") or {}).get("kernel","")[:40])
+PY
