@@ -148,7 +148,9 @@ typedef struct {
                                   256, 512} (every BSMR tile on MFMA, a panel's A rows staged once
                                   per item): 0 never, 1 whenever dtype and K allow, -1 = auto
                                   (tile-dominated plans, e.g. 16 x 16 block masks) */
-    int32_t ptile_tpi;         /* BSMR_PTILE_TPI: tiles per panel-tile item, 1..64; -1 = 4 */
+    int32_t ptile_tpi;         /* BSMR_PTILE_TPI: 0 = equal tile runs, one per CU, of up to two
+                                  panels each; 1..64 = items of at most that many tiles of one
+                                  panel; -1 = 0 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

@@ -145,7 +145,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->pair_min_items >= 0) p.pair_min_items = static_cast<u32>(t->pair_min_items);
         if (t->batches >= 0) p.batches = t->batches ? 1 : 0;
         if (t->ptile >= 0) p.ptile_mode = t->ptile ? 1 : 0;
-        if (t->ptile_tpi > 0) p.ptile_tpi = static_cast<u32>(std::min(64, t->ptile_tpi));
+        if (t->ptile_tpi >= 0) p.ptile_tpi = static_cast<u32>(std::min(64, t->ptile_tpi));
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;

@@ -1,6 +1,7 @@
 // plan.hpp — the device-resident BSMR plan (reference BSMR + RPHM, include/BSMR.hpp:21-159).
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -271,15 +272,21 @@ struct Plan {
     // K in {64, 128, 256, 512}; items {panel, first tile, tiles <= tpi, 0} in launch order
     struct PtileLayout {
         bool built = false;
-        u32 tpi = 0, nItems = 0, nListed = 0;
+        u32 tpi = 0, nItems = 0, nListed = 0, waves = 8, stride = 0;
+        // per item slot {first panel, first tile, tiles, second panel + 1 (0: one panel)}
         DevBuf<uint4> items;
-        // per item slot: 16 A rows, first tile, tiles, 14 zeros, 16 columns per tile (tpi slots)
+        // per item slot (stride u32): 32 A rows (the first panel's 16, then the second's, or the
+        // first's again), {first tile, tiles, tiles of the first panel, panels}, 12 zeros, 16
+        // columns per tile (a block for every tile and at least one per wave)
         DevBuf<u32> desc;
-        static u32 desc_stride(u32 tpi) { return 32 + 16 * tpi; }
+        static u32 desc_waves(u32 tpi) { return tpi > 0 && tpi <= 4 ? 4u : 8u; }
+        static u32 desc_stride(u32 tiles) { return 48 + 16 * tiles; }
     };
     mutable PtileLayout ptile;
     int ptile_mode = -1;  // BSMR_PTILE: 0 never, 1 whenever it applies, -1 auto
-    u32 ptile_tpi = 4;    // BSMR_PTILE_TPI: tiles per item (C5 block: 4 -> 6.3 us, 8 -> 9.7, 2 -> 6.6)
+    // BSMR_PTILE_TPI: 0 = equal tile runs, one per CU (up to two panels each); n > 0 = items of
+    // at most n tiles of one panel (C5 block: 4 -> 5.93 us, 2 -> 7.5, 5 -> 7.7)
+    u32 ptile_tpi = 0;
     int build_ptile_layout(u32 tpi) const;
 
     int build_rows(const u32* h_rowptr, const u32* h_col);

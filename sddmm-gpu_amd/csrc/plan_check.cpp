@@ -635,47 +635,56 @@ private:
     }
 
     // column-major launch (k_sddmm_f32 / k_sddmm_half): every tile + residual slots
-    // the panel-grouped tile launch: every tile id in exactly one item, inside the item's panel
-    // (its A rows are the panel's 16 reordered rows), at most tpi per item; then the residual
+    // the panel-grouped tile launch: every tile id in exactly one item; an item's tiles are one
+    // contiguous run inside its first panel, or inside its first and second panel with no tile of
+    // a third between them (its A rows are those panels' 16 reordered rows each), at most tpi
+    // tiles of one panel when tpi > 0; the descriptors the kernel reads agree; then the residual
     // slots as in the column-major launch
     int ptile_layout(bool* ok) {
         const Plan& p_ = *pp_;
+        const Plan::PtileLayout& PL = p_.ptile;
         std::vector<uint4> items;
-        BSMR_CHECK(p_.ptile.items.download(items, p_.stream));
-        items.resize(p_.ptile.nItems);
-        *ok = false;
-        const u32 nt = static_cast<u32>(h_.bv.size() / TILE);
-        std::vector<uint8_t> thit(std::max<u32>(nt, 1), 0);
-        if (p_.ptile.nItems % XCD_BUCKETS)
-            return layout_fail(fmt("panel-tile launch: %u item slots, not a multiple of 8", p_.ptile.nItems)), BSMR_OK;
-        for (u32 i = 0; i < p_.ptile.nItems; ++i) {
-            const uint4 it = items[i];
-            if (it.z == 0) continue;
-            if (it.x >= h_.P || it.z > p_.ptile.tpi || it.y < h_.bo[it.x] || it.y + it.z > h_.bo[it.x + 1])
-                return layout_fail(fmt("panel-tile item %u {panel %u, tile %u, %u tiles} outside its panel", i, it.x, it.y, it.z)), BSMR_OK;
-            for (u32 t = it.y; t < it.y + it.z; ++t)
-                if (thit[t]++) return layout_fail(fmt("panel-tile: tile %u in two items", t)), BSMR_OK;
-        }
-        // the descriptors the kernel reads: the item's panel rows, tile range and tile columns
+        BSMR_CHECK(PL.items.download(items, p_.stream));
+        items.resize(PL.nItems);
         std::vector<u32> desc;
-        BSMR_CHECK(p_.ptile.desc.download(desc, p_.stream));
-        const u32 ds = Plan::PtileLayout::desc_stride(p_.ptile.tpi);
-        if (desc.size() < static_cast<size_t>(p_.ptile.nItems) * ds)
+        BSMR_CHECK(PL.desc.download(desc, p_.stream));
+        *ok = false;
+        const u32 nt = static_cast<u32>(h_.bv.size() / TILE), ds = PL.stride;
+        std::vector<uint8_t> thit(std::max<u32>(nt, 1), 0);
+        if (PL.nItems % XCD_BUCKETS)
+            return layout_fail(fmt("panel-tile launch: %u item slots, not a multiple of 8", PL.nItems)), BSMR_OK;
+        if (desc.size() < static_cast<size_t>(PL.nItems) * ds || ds < 48)
             return layout_fail("panel-tile descriptors missing"), BSMR_OK;
-        for (u32 i = 0; i < p_.ptile.nItems; ++i) {
+        for (u32 i = 0; i < PL.nItems; ++i) {
             const uint4 it = items[i];
             const u32* d = desc.data() + static_cast<size_t>(i) * ds;
-            if (d[17] != it.z || (it.z && d[16] != it.y))
-                return layout_fail(fmt("panel-tile descriptor %u: tiles [%u, +%u) for item [%u, +%u)", i, d[16], d[17], it.y, it.z)), BSMR_OK;
-            for (u32 r = 0; r < 16 && it.z; ++r) {
-                const u32 x = 16 * it.x + r, want = x < h_.R ? h_.rows[x] : h_.rows[0];
+            if (it.z == 0) {
+                if (d[33] != 0) return layout_fail(fmt("panel-tile descriptor %u: tiles in a padding slot", i)), BSMR_OK;
+                continue;
+            }
+            const u32 q0 = it.x, two = it.w != 0, q1 = two ? it.w - 1 : q0;
+            const u32 t0 = it.y, t1 = it.y + it.z;
+            const bool inside = q0 < h_.P && q1 < h_.P && t0 >= h_.bo[q0] &&
+                                (two ? q1 > q0 && h_.bo[q0 + 1] == h_.bo[q1] && t0 < h_.bo[q0 + 1] &&
+                                           t1 > h_.bo[q1] && t1 <= h_.bo[q1 + 1]
+                                     : t1 <= h_.bo[q0 + 1]);
+            if (!inside || (PL.tpi > 0 && (two || it.z > PL.tpi)) || 48 + 16 * it.z > ds)
+                return layout_fail(fmt("panel-tile item %u {panels %u..%u, tiles [%u, %u)} outside its panels", i, q0, q1, t0, t1)), BSMR_OK;
+            for (u32 t = t0; t < t1; ++t)
+                if (thit[t]++) return layout_fail(fmt("panel-tile: tile %u in two items", t)), BSMR_OK;
+            // the descriptor
+            const u32 n0 = two ? h_.bo[q0 + 1] - t0 : it.z;
+            if (d[32] != t0 || d[33] != it.z || d[34] != n0 || d[35] != (two ? 2u : 1u))
+                return layout_fail(fmt("panel-tile descriptor %u: tiles [%u, +%u) split %u panels %u for item [%u, +%u)", i, d[32], d[33], d[34], d[35], t0, it.z)), BSMR_OK;
+            for (u32 r = 0; r < 32; ++r) {
+                const u32 x = 16 * (r < 16 ? q0 : q1) + (r & 15), want = x < h_.R ? h_.rows[x] : h_.rows[0];
                 if (d[r] != want)
                     return layout_fail(fmt("panel-tile descriptor %u: row %u is %u, panel row %u", i, r, d[r], want)), BSMR_OK;
             }
             for (u32 j = 0; j < it.z; ++j)
                 for (u32 c = 0; c < 16; ++c)
-                    if (d[32 + 16 * j + c] != h_.dcols[static_cast<size_t>(it.y + j) * 16 + c])
-                        return layout_fail(fmt("panel-tile descriptor %u: column %u of tile %u", i, c, it.y + j)), BSMR_OK;
+                    if (d[48 + 16 * j + c] != h_.dcols[static_cast<size_t>(t0 + j) * 16 + c])
+                        return layout_fail(fmt("panel-tile descriptor %u: column %u of tile %u", i, c, t0 + j)), BSMR_OK;
         }
         for (u32 t = 0; t < nt; ++t)
             if (!thit[t]) return layout_fail(fmt("panel-tile: tile %u in no item", t)), BSMR_OK;

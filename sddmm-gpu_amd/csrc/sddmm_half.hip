@@ -204,7 +204,8 @@ template <bool BF16, u32 NK, u32 NW>
 __global__ __launch_bounds__(64 * NW) void k_sddmm_ptile(PtileArgs a) {
     static_assert(NK == 2 || NK == 4 || NK == 8 || NK == 16, "K / 32 in {2, 4, 8, 16}");
     constexpr u32 NT = 64 * NW;
-    __shared__ __attribute__((aligned(16))) s16x8 sa[16 * 4 * NK];
+    // the A image: up to two panels (32 rows) of the item
+    __shared__ __attribute__((aligned(16))) s16x8 sa[32 * 4 * NK];
     if (blockIdx.y) {
         a.h.A += blockIdx.y * a.h.bA;
         a.h.B += blockIdx.y * a.h.bB;
@@ -221,21 +222,36 @@ __global__ __launch_bounds__(64 * NW) void k_sddmm_ptile(PtileArgs a) {
         return;
     }
     const unsigned long long t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    // the item's descriptor: rows d[0..16), first tile d[16], tiles d[17], columns d[32 + 16 j + c]
+    // the item's descriptor (PtileLayout): rows d[0..32) (panel 0's 16, then panel 1's), {first
+    // tile, tiles, tiles of panel 0, panels} at d[32..36), columns d[48 + 16 j + c]
     const u32* const d = a.desc + static_cast<size_t>(b) * a.dstride;
-    const u32 t0 = d[16], nt = d[17];
-    if (nt == 0) return;  // uniform: padding slot
-    const u32 K = 32 * NK;
     const u32 rr = lane & 15, g = lane >> 4;
+    constexpr u32 CPR = 4 * NK, NCH = 32 * CPR, PER = (NCH + NT - 1) / NT;
+    // round trip 1, every descriptor load at once: the rows of this thread's A chunks, the
+    // columns of the wave's first tile, the tile range (a padding slot's descriptor is zeros)
+    u32 arow[PER];
+#pragma unroll
+    for (u32 i = 0; i < PER; ++i) {
+        const u32 f = tid + NT * i;
+        arow[i] = (NCH % NT == 0 || f < NCH) ? d[f / CPR] : 0u;
+    }
+    const u32 cfirst = d[48 + 16 * w + rr];
+    const uint4 hd = *reinterpret_cast<const uint4*>(d + 32);
+    const u32 t0 = __builtin_amdgcn_readfirstlane(hd.x), nt = __builtin_amdgcn_readfirstlane(hd.y);
+    const u32 n0 = __builtin_amdgcn_readfirstlane(hd.z), np = __builtin_amdgcn_readfirstlane(hd.w);
+    // (no early return for a padding slot, nt = 0: a branch here would hold every other load of
+    // the prologue behind the tile count's round trip; it loads row 0 and tile t0 = 0 and stores
+    // nothing)
+    const u32 K = 32 * NK;
     const size_t rowB = static_cast<size_t>(K) * 2;
     const char* const Ab = reinterpret_cast<const char*>(a.h.A);
     const char* const Bb = reinterpret_cast<const char*>(a.h.B);
     // the wave's tile j: B fragments (one 16-byte load per k-step) and its four output positions
     s16x8 bf[NK];
     u32 idx[4];
-    auto load_tile = [&](const u32 j) {
-        const u32 tile = t0 + j;
-        const u32 c = d[32 + 16 * j + rr];
+    auto load_tile = [&](const u32 j, const u32 c) {
+        // (a wave past the item's tiles, or of a padding slot, loads a real tile and stores nothing)
+        const u32 tile = t0 + min(j, max(nt, 1u) - 1);
         const char* bp = Bb + static_cast<size_t>(c < a.h.N ? c : 0) * rowB + 16 * g;
 #pragma unroll
         for (u32 s = 0; s < NK; ++s) bf[s] = *reinterpret_cast<const s16x8*>(bp + 64 * s);
@@ -243,34 +259,34 @@ __global__ __launch_bounds__(64 * NW) void k_sddmm_ptile(PtileArgs a) {
 #pragma unroll
         for (u32 r = 0; r < 4; ++r) idx[r] = bv[16 * r];
     };
-    // the first tile's loads go out ahead of the A staging (their latency overlaps it)
-    if (w < nt) load_tile(w);
-    // the panel's A rows: 64 NK chunks of 16 bytes, thread tid takes chunks tid, tid + NT, ...
-    constexpr u32 CPR = 4 * NK, NCH = 16 * CPR, PER = (NCH + NT - 1) / NT;
+    // round trip 2: the item's A rows (chunks of the second panel only when it has one; thread tid
+    // takes chunks tid, tid + NT, ...), then the first tile's B fragments and output positions;
+    // the A data's wait leaves the B loads in flight across the barrier
+    const u32 lim = (np > 1 ? 32u : 16u) * CPR;
     s16x8 av[PER];
 #pragma unroll
     for (u32 i = 0; i < PER; ++i) {
         const u32 f = tid + NT * i;
-        if (NCH % NT == 0 || f < NCH) {
-            const u32 r = f / CPR, c = f % CPR, row = d[r];
-            av[i] = *reinterpret_cast<const s16x8*>(Ab + static_cast<size_t>(row) * rowB + 16 * c);
-        }
+        if (f < lim)
+            av[i] = *reinterpret_cast<const s16x8*>(Ab + static_cast<size_t>(arow[i]) * rowB + 16 * (f % CPR));
     }
+    load_tile(w, cfirst);
 #pragma unroll
     for (u32 i = 0; i < PER; ++i) {
         const u32 f = tid + NT * i;
-        if (NCH % NT == 0 || f < NCH) sa[ptile_slot<NK>(f / CPR, f % CPR)] = av[i];
+        if (f < lim) sa[ptile_slot<NK>(f / CPR, f % CPR)] = av[i];
     }
     __syncthreads();
     const unsigned long long t_mid = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     unsigned long long t_mfma = 0;
     // one tile per wave at a time (NK 16-byte B loads in flight per lane): NK MFMAs with A
-    // fragments from LDS, then the scatter
+    // fragments from its panel's rows in LDS, then the scatter
     for (u32 j = w; j < nt; j += NW) {
-        if (j != w) load_tile(j);
+        if (j != w) load_tile(j, d[48 + 16 * j + rr]);
+        const u32 ra = (j < n0 ? 0u : 16u) + rr;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (u32 s = 0; s < NK; ++s) acc = mfma32<BF16>(sa[ptile_slot<NK>(rr, 4 * s + g)], bf[s], acc);
+        for (u32 s = 0; s < NK; ++s) acc = mfma32<BF16>(sa[ptile_slot<NK>(ra, 4 * s + g)], bf[s], acc);
         if (a.trace && j == w)  // (reads the result: after the last MFMA)
             t_mfma = __builtin_amdgcn_s_memrealtime() + (acc[0] != acc[0] ? 1ull : 0ull);
 #pragma unroll
@@ -290,54 +306,92 @@ __global__ __launch_bounds__(64 * NW) void k_sddmm_ptile(PtileArgs a) {
 
 }  // namespace
 
-// Items of the panel-grouped tile launch (built on first use, per tiles-per-item): every panel's
-// tiles cut into runs of <= tpi; the list is dealt as contiguous eighths per XCD (slot b on XCD
-// b % 8 takes list position (b % 8) per + b / 8), so an XCD's panels are neighbours.
+// Items of the panel-grouped tile launch (built on first use). By default (tpi = 0) the tiles,
+// in plan order, are cut into as many equal runs as the chip has CUs (runs of at most 8 tiles
+// when there are more), a run crossing a panel boundary taking both panels' A rows (a run that
+// would need a third panel is split): every CU then stages about the same bytes — 16 B rows per
+// tile plus 16 A rows per panel — in one round. With tpi > 0 (BSMR_PTILE_TPI) every panel's tiles
+// are cut into ceil(n / tpi) near-equal items of one panel. The list is dealt as contiguous
+// eighths per XCD (slot b on XCD b % 8 takes list position (b % 8) per + b / 8).
 int Plan::build_ptile_layout(u32 tpi) const {
     PtileLayout& L = ptile;
-    // a panel of n tiles: ceil(n / tpi) items of near-equal size (13 at tpi 4: 4, 3, 3, 3)
-    std::vector<uint4> list;
-    for (u32 q = 0; q < P; ++q) {
-        const u32 a = h_blockOffsets[q], n = h_blockOffsets[q + 1] - a, k = (n + tpi - 1) / tpi;
-        for (u32 i = 0; i < k; ++i) {
-            const u32 t0 = a + static_cast<u32>(static_cast<u64>(n) * i / k);
-            const u32 t1 = a + static_cast<u32>(static_cast<u64>(n) * (i + 1) / k);
-            list.push_back(make_uint4(q, t0, t1 - t0, 0));
+    struct It {
+        u32 q0, q1, t0, nt, n0;  // panels q0 (and q1 when n0 < nt), tiles [t0, t0 + nt)
+    };
+    std::vector<It> list;
+    const u32 T = h_blockOffsets[P];
+    const auto panel_of = [&](u32 t) {  // the panel holding tile t (empty panels skipped)
+        return static_cast<u32>(std::upper_bound(h_blockOffsets.begin(), h_blockOffsets.begin() + P + 1, t) -
+                                h_blockOffsets.begin()) - 1;
+    };
+    u32 maxTiles = 0;
+    if (tpi > 0) {
+        for (u32 q = 0; q < P; ++q) {
+            const u32 a = h_blockOffsets[q], n = h_blockOffsets[q + 1] - a, k = (n + tpi - 1) / tpi;
+            for (u32 i = 0; i < k; ++i) {
+                const u32 t0 = a + static_cast<u32>(static_cast<u64>(n) * i / k);
+                const u32 t1 = a + static_cast<u32>(static_cast<u64>(n) * (i + 1) / k);
+                list.push_back({q, q, t0, t1 - t0, t1 - t0});
+            }
+        }
+    } else if (T > 0) {
+        int cus = 256;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+            cus = 256;
+        const u32 nb = std::max<u32>(static_cast<u32>(cus), (T + 7) / 8);
+        for (u32 k = 0; k < nb; ++k) {
+            const u32 a = static_cast<u32>(static_cast<u64>(T) * k / nb);
+            const u32 e = static_cast<u32>(static_cast<u64>(T) * (k + 1) / nb);
+            for (u32 t = a; t < e;) {
+                const u32 q0 = panel_of(t), e0 = std::min(h_blockOffsets[q0 + 1], e);
+                if (e0 == e) {
+                    list.push_back({q0, q0, t, e - t, e - t});
+                    t = e;
+                } else {
+                    const u32 q1 = panel_of(e0), e1 = std::min(h_blockOffsets[q1 + 1], e);
+                    list.push_back({q0, q1, t, e1 - t, e0 - t});
+                    t = e1;
+                }
+            }
         }
     }
+    for (const It& it : list) maxTiles = std::max(maxTiles, it.nt);
     const u32 n = static_cast<u32>(list.size());
     const u32 per = (n + XCD_BUCKETS - 1) / XCD_BUCKETS;
-    std::vector<uint4> slots(static_cast<size_t>(per) * XCD_BUCKETS, make_uint4(0, 0, 0, 0));
-    for (u32 b = 0; b < slots.size(); ++b) {
-        const u32 pos = (b % XCD_BUCKETS) * per + b / XCD_BUCKETS;
-        if (pos < n) slots[b] = list[pos];
-    }
-    // per item slot its descriptor (PtileArgs::desc): the panel's 16 A rows, the first tile and the
-    // tile count, then 16 columns per tile — what the kernel's loads need, one load away
+    const u32 nslots = per * XCD_BUCKETS;
+    // the descriptors (PtileArgs::desc): per item slot its rows, header and tile columns
     std::vector<u32> hrows, hcols;
     BSMR_CHECK(rows.download(hrows, stream));
     BSMR_CHECK(denseCols.download(hcols, stream));
-    const u32 ds = PtileLayout::desc_stride(tpi);
-    std::vector<u32> desc(static_cast<size_t>(slots.size()) * ds, 0);
-    for (size_t b = 0; b < slots.size(); ++b) {
-        const uint4 it = slots[b];
-        u32* d = desc.data() + b * ds;
-        if (it.z == 0) continue;
-        for (u32 r = 0; r < 16; ++r) {
-            const u32 x = 16 * it.x + r;
+    const u32 waves = PtileLayout::desc_waves(tpi);
+    const u32 ds = PtileLayout::desc_stride(std::max(maxTiles, waves));
+    std::vector<u32> desc(static_cast<size_t>(nslots) * ds, 0);
+    std::vector<uint4> items(std::max<u32>(nslots, 1), make_uint4(0, 0, 0, 0));
+    for (u32 b = 0; b < nslots; ++b) {
+        const u32 pos = (b % XCD_BUCKETS) * per + b / XCD_BUCKETS;
+        if (pos >= n) continue;
+        const It& it = list[pos];
+        items[b] = make_uint4(it.q0, it.t0, it.nt, it.n0 < it.nt ? it.q1 + 1 : 0u);
+        u32* d = desc.data() + static_cast<size_t>(b) * ds;
+        for (u32 r = 0; r < 32; ++r) {
+            const u32 x = 16 * (r < 16 || it.n0 == it.nt ? it.q0 : it.q1) + (r & 15);
             d[r] = x < R ? hrows[x] : hrows[0];
         }
-        d[16] = it.y;
-        d[17] = it.z;
-        for (u32 j = 0; j < it.z; ++j)
-            for (u32 c = 0; c < 16; ++c) d[32 + 16 * j + c] = hcols[(it.y + j) * 16 + c];
+        d[32] = it.t0;
+        d[33] = it.nt;
+        d[34] = it.n0;
+        d[35] = it.n0 < it.nt ? 2u : 1u;
+        for (u32 j = 0; j < it.nt; ++j)
+            for (u32 c = 0; c < 16; ++c) d[48 + 16 * j + c] = hcols[(it.t0 + j) * 16 + c];
     }
-    BSMR_CHECK(L.items.upload(slots.data(), std::max<size_t>(slots.size(), 1), stream));
+    BSMR_CHECK(L.items.upload(items.data(), items.size(), stream));
     BSMR_CHECK(L.desc.upload(desc.data(), std::max<size_t>(desc.size(), 1), stream));
     BSMR_HIP(hipStreamSynchronize(stream));  // host vectors are pageable memory
-    L.nItems = static_cast<u32>(slots.size());
+    L.nItems = nslots;
     L.nListed = n;
     L.tpi = tpi;
+    L.waves = waves;
+    L.stride = ds;
     L.built = true;
     return BSMR_OK;
 }
@@ -372,7 +426,7 @@ int launch_ptile(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     a.h.bB = static_cast<unsigned long long>(p.N) * K;
     a.h.bP = p.nnz;
     a.desc = p.ptile.desc.data();
-    a.dstride = Plan::PtileLayout::desc_stride(p.ptile.tpi);
+    a.dstride = p.ptile.stride;
     a.nItems = (mode & 1) ? p.ptile.nItems : 0;
     a.trace = nullptr;
     u32 grid = a.nItems + (a.h.nslots + 3) / 4;
@@ -387,7 +441,7 @@ int launch_ptile(const Plan& p, const void* dA, const void* dB, u32 K, int dtype
     const bool bf = dtype == BSMR_BF16;
     const dim3 gd(grid, nb);
     // waves per workgroup: one per tile of an item up to 8 (items of more tiles loop)
-    const bool w8 = p.ptile.tpi > 4;
+    const bool w8 = p.ptile.waves == 8;
 #define BSMR_PT(NKV) (w8 ? (bf ? k_sddmm_ptile<true, NKV, 8> : k_sddmm_ptile<false, NKV, 8>) \
                          : (bf ? k_sddmm_ptile<true, NKV, 4> : k_sddmm_ptile<false, NKV, 4>))
     void (*fn)(PtileArgs) = NK == 2 ? BSMR_PT(2) : NK == 4 ? BSMR_PT(4) : NK == 8 ? BSMR_PT(8) : BSMR_PT(16);

@@ -48,10 +48,10 @@ def test_block_mask_every_tile_on_mfma(K, dtype):
     assert plan.check(K, dtype, verbose=False) == (True, "")
 
 
-@pytest.mark.parametrize("tpi", [1, 3, 8, 64])
+@pytest.mark.parametrize("tpi", [0, 1, 3, 8, 64])
 def test_tiles_per_item(tpi):
-    """Items of 1..64 tiles of one panel: 4 or 8 waves per workgroup, looping over the item's
-    tiles past one per wave."""
+    """Items of 1..64 tiles of one panel (4 or 8 waves per workgroup, looping over the item's
+    tiles past one per wave), and the default equal runs of up to two panels (tpi 0)."""
     M, N, rp, ci = synth.block_mask(768, 16, 0.2, seed=12)
     plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE,
                 tuning={"ptile_tpi": tpi})
@@ -120,8 +120,22 @@ def test_corrupted_descriptor_fails_the_layout_check(word):
     items = plan.stats()["ptile_items"]
     assert items > 0
     # the first item slot with tiles (slot 0 holds the XCD-0 eighth's first item)
-    idx = {"row": 3, "column": 32 + 5, "tiles": 17}[word]
+    idx = {"row": 3, "column": 48 + 5, "tiles": 33}[word]
     old = _poke(plan, 103, idx, 7, 256, 2)
     _poke(plan, 103, idx, old ^ 1 if word != "tiles" else old + 1, 256, 2)
     ok, msg = plan.check(256, 2, verbose=False)
     assert not ok and "panel-tile descriptor" in msg, msg
+
+
+@pytest.mark.parametrize("scale", [1, 3])
+def test_equal_runs_across_panel_boundaries(scale):
+    """The default item list (equal tile runs, one per CU): with more tiles than CUs most runs
+    cross a panel boundary and stage both panels' A rows (32 rows in LDS, the second panel's
+    tiles reading rows 16..31); with 3x the tiles of C5 a run holds up to 8 tiles (more runs than
+    CUs). Every output equals the oracle's, and the layout check covers both panels' rows."""
+    M, N, rp, ci = synth.block_mask(1024 * scale, 16, 0.1, seed=16)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    st = plan.stats()
+    assert st["num_residual"] == 0 and st["num_dense_tiles"] > 256
+    _check(plan, M, N, rp, ci, 512, 2)
+    assert plan.check(512, 2, verbose=False) == (True, "")

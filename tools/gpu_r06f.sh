@@ -1,0 +1,21 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r06f; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_ptile.py -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest.log; exit 1; }
+TR="python3 tools/trace_sddmm.py"
+timeout -k 10 300 $TR --workload dlmc_like --mask block --K 512 --dtype bf16 --waves-per-wg 1 > $O/trace_ptile_bins.json 2> $O/trace_ptile_bins.err || exit 2
+Q="--no-cpu-baseline --no-vendor --pmc off --config C5 --steps 100 --warmup 10"
+run() { local name=$1; shift; env "$@" timeout -k 10 300 python3 bench.py $Q $EXTRA > $O/$name.json 2> $O/$name.err || exit 3; }
+EXTRA="--mask block" run blk_bins BSMR_PTILE=-1
+EXTRA="--mask block" run blk_tpi4 BSMR_PTILE_TPI=4
+EXTRA="--mask block" run blk_bins2 BSMR_PTILE=-1
+EXTRA="--mask block" run blk_tpi4b BSMR_PTILE_TPI=4
+EXTRA="--mask block" run blk_off BSMR_PTILE=0
+for K in 128 256; do EXTRA="--mask block --K $K" run blk_K${K} BSMR_PTILE=-1; EXTRA="--mask block --K $K" run blk_K${K}_tpi4 BSMR_PTILE_TPI=4; done
+python3 - <<'PY'
+import json,glob
+for f in sorted(glob.glob("gpurun_out/r06f/*.json")):
+    d=json.load(open(f))
+    if "value" in d: print(f.split('/')[-1], d.get("value"), d.get("ms_per_step"))
+    else: print(f.split('/')[-1], {k: d.get(k) for k in ("span_us","start_us","mid_us","end_us")})
+PY

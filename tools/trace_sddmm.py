@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
     ap.add_argument("--waves-per-wg", type=int, default=16, help="NT / 64 of the traced launch")
     ap.add_argument("--mask", default=None, help="dlmc_like mask: uniform | block")
+    ap.add_argument("--cold", action="store_true",
+                    help="trace a launch right after a 512 MiB write (Infinity Cache evicted, as "
+                         "bench.py's cold leg)")
     args = ap.parse_args()
     os.environ["BSMR_DIAG"] = str(int(os.environ.get("BSMR_DIAG", "0")) | 32)
     import torch
@@ -55,6 +58,12 @@ def main():
     for _ in range(10):
         plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s, dtype=code)
     torch.cuda.synchronize()
+    if args.cold:  # evict the MALL, then the traced launch
+        flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+        flush.fill_(1)
+        torch.cuda.synchronize()
+        plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s, dtype=code)
+        torch.cuda.synchronize()
     L = bsmr.lib()
     L.bsmr_debug_trace.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
     n = C.c_uint64()
@@ -73,6 +82,7 @@ def main():
     us = 0.01  # 100 MHz ticks -> us
     xcc = (t[:, 3] >> np.uint64(60)).astype(np.int64) & 0xF
     out = {"K": K, "workload": args.workload, "dtype": args.dtype, "layout": args.layout,
+           "cold": args.cold,
            "lds_kb": args.lds_kb, "waves": int(len(t)),
            "rb": {k: plan.stats()[k] for k in ("rb_rows", "rb_items", "rb_pieces")},
            "span_us": round(float((t1.max() - base) * us), 3),
