@@ -431,8 +431,9 @@ def kernel_name(st, st_after, K, dtype, layout):
     rby = K * (4 if dtype == F32 else 2)
     if st_after.get("ptile_items"):  # sddmm.hip use_ptile (its item list is built on first use)
         return (f"k_sddmm_ptile<{'f16' if dtype == 1 else 'bf16'},{K // 32}> (panel-grouped BSMR "
-                f"tiles, every tile on MFMA 16x16x32: a panel's 16 A rows staged in LDS once per "
-                f"item, {st_after['ptile_items']} item slots; residual in column-major slots)"), rby
+                f"tiles, every tile on MFMA 16x16x32: equal tile runs, one per CU, their panels' A "
+                f"rows staged in LDS once, {st_after['ptile_items']} item slots; residual in "
+                f"column-major slots)"), rby
     tile_dominated = st["num_residual"] * 4 < st["num_dense_tiles"] * 16  # sddmm.hip rb_slot
     if rby in (128, 256, 512, 1024, 2048) and layout != "colmajor" and not tile_dominated:
         tiles = ("fp32 tiles demoted to residual entries" if dtype == F32

@@ -32,7 +32,7 @@ extern "C" {
                               bsmr_tuning.pair_min_items, stats rb_pairs;
                               11: bsmr_tuning.batches, stats rb_batches;
                               12: bsmr_tuning.ptile / ptile_tpi (panel-grouped fp16/bf16 tile
-                              launch), stats ptile_items, bsmr_cost_cuts; removed the dropped experiments'
+                              launch), piece_balance, stats ptile_items, bsmr_cost_cuts; removed the dropped experiments'
                               knobs piece_order, seg_items, sweep* and stats rb_sweep */
 
 typedef enum {
@@ -151,6 +151,10 @@ typedef struct {
     int32_t ptile_tpi;         /* BSMR_PTILE_TPI: 0 = equal tile runs, one per CU, of up to two
                                   panels each; 1..64 = items of at most that many tiles of one
                                   panel; -1 = 0 */
+    int32_t piece_balance;     /* BSMR_PIECE_BALANCE: row-block items without dynamic batches place
+                                  their pieces so that the waves' phase costs even out (runs of
+                                  the longest-first list dealt to the least-loaded wave) instead of
+                                  longest first in position order; 0 never, 1 always, -1 = auto */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

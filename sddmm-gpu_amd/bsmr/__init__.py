@@ -49,7 +49,8 @@ class Tuning(C.Structure):
                 ("rb_rows", C.c_int32), ("late_b", C.c_int32), ("item_cap", C.c_float),
                 ("item_sched", C.c_int32), ("out_packed", C.c_int32),
                 ("cluster_filter", C.c_int32), ("pair_min_items", C.c_int32),
-                ("batches", C.c_int32), ("ptile", C.c_int32), ("ptile_tpi", C.c_int32)]
+                ("batches", C.c_int32), ("ptile", C.c_int32), ("ptile_tpi", C.c_int32),
+                ("piece_balance", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -248,7 +249,7 @@ def tuning_from_env(env=None):
         if v is None:
             continue
         if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "cluster_filter",
-                 "batches", "ptile"):  # tri-state: "0" never, "1" always, else auto
+                 "batches", "ptile", "piece_balance"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
         elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap"):
             out[f] = float(v)

@@ -39,6 +39,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->pair_min_items = -1;
     t->batches = -1;
     t->ptile = t->ptile_tpi = -1;
+    t->piece_balance = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -89,6 +90,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     get3("BSMR_BATCHES", t->batches);
     get3("BSMR_PTILE", t->ptile);
     geti("BSMR_PTILE_TPI", t->ptile_tpi);
+    get3("BSMR_PIECE_BALANCE", t->piece_balance);
     return n;
 }
 
@@ -146,6 +148,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->batches >= 0) p.batches = t->batches ? 1 : 0;
         if (t->ptile >= 0) p.ptile_mode = t->ptile ? 1 : 0;
         if (t->ptile_tpi >= 0) p.ptile_tpi = static_cast<u32>(std::min(64, t->ptile_tpi));
+        if (t->piece_balance >= 0) p.piece_balance = t->piece_balance ? 1 : 0;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;

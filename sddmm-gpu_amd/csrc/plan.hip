@@ -1575,6 +1575,52 @@ static void par_for(size_t n, F&& f, size_t serial_below = 2048) {
     for (auto& x : th) x.join();
 }
 
+// Static piece order of one row-block item (Plan::piece_balance). The kernel deals phase ph's
+// pieces [ph NG, (ph + 1) NG) to row-groups gr, reversed in odd phases (sddmm.hip: piece
+// ph NG + (ph odd ? NG - 1 - gr : gr)); a wave's 64 / G row-groups run a phase in lockstep, so a
+// wave pays per phase its longest piece plus one gather (w entry-steps, the item cost model's
+// piece weight). With the pieces longest first in position order, the waves that also run the
+// short last phase end last. Here the same pieces, sorted longest first, go out in runs — one
+// run per (wave, phase) bucket, as many pieces as that bucket has positions — always to the wave
+// whose running cost is lowest (LPT over the buckets), so waves with two phases get shorter runs.
+static void balance_pieces(std::vector<uint2>& pcs, u32 NT, u32 G, double w) {
+    const u32 NG = NT / G, GW = 64 / G, NW = NT / 64;
+    const u32 np = static_cast<u32>(pcs.size());
+    if (np <= NG) return;  // one phase: every wave has one bucket already in cost order
+    const u32 nph = (np + NG - 1) / NG;
+    struct Bucket {
+        u32 ph, cap;
+        std::vector<u32> pos;  // the positions (piece indices) of its row-groups
+    };
+    std::vector<std::vector<Bucket>> wb(NW);
+    for (u32 ph = 0; ph < nph; ++ph)
+        for (u32 wv = 0; wv < NW; ++wv) {
+            Bucket bk{ph, 0, {}};
+            for (u32 gr = wv * GW; gr < (wv + 1) * GW; ++gr) {
+                const u32 pos = ph * NG + ((ph & 1) ? NG - 1 - gr : gr);
+                if (pos < np) bk.pos.push_back(pos);
+            }
+            bk.cap = static_cast<u32>(bk.pos.size());
+            if (bk.cap) wb[wv].push_back(std::move(bk));
+        }
+    // buckets of a wave largest first
+    for (auto& v : wb)
+        std::stable_sort(v.begin(), v.end(), [](const Bucket& a, const Bucket& b) { return a.cap > b.cap; });
+    std::vector<double> cost(NW, 0.0);
+    std::vector<u32> next(NW, 0);
+    std::vector<uint2> out(np);
+    u32 k = 0;  // pcs sorted longest first
+    while (k < np) {
+        u32 best = NW;
+        for (u32 wv = 0; wv < NW; ++wv)
+            if (next[wv] < wb[wv].size() && (best == NW || cost[wv] < cost[best])) best = wv;
+        const Bucket& bk = wb[best][next[best]++];
+        cost[best] += static_cast<double>((pcs[k].y >> 22) + 1) + w;
+        for (u32 pos : bk.pos) out[pos] = pcs[k++];
+    }
+    pcs.swap(out);
+}
+
 int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
                                 bool orig) const {
     L.rowBytes = 0;
@@ -2131,6 +2177,36 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                              [](const uint2& a, const uint2& b) { return (a.y >> 22) > (b.y >> 22); });
         }
     });
+    // dynamic piece batches (Plan::batches; kernels for rows of <= 512 B): after its first batch
+    // of 64 / G pieces a wave takes the next from an LDS counter, which balances the waves of
+    // items with several pieces per row-group. Measured (profiles/r05bt, forced on against off):
+    // 512-byte rows with 2.4 / 6.5 / 6.8 pieces per row-group (mycielskian14 K = 128, C3, C4
+    // x0.5) -4.5 / -2.4 / -2.2 %, C2's 1.4 +5 %; 128- and 256-byte rows (mycielskian15 K = 32,
+    // Trefethen K = 64: little work per entry behind each counter round trip) +2 to +8 %. Auto:
+    // 512-byte rows from batch_min_phases pieces per row-group
+    bool dyn = false;
+    {
+        u64 npAll = 0;
+        u32 nWork = 0;
+        for (size_t i = 0; i < items.size(); ++i) {
+            npAll += ipc[i].size();
+            nWork += !(items[i].y == items[i].z && items[i].w == ends[i]);
+        }
+        const u32 NGl = NT / 4;  // row-groups (G = 4 for rows of <= 512 B)
+        const double perItem = nWork ? static_cast<double>(npAll) / nWork : 0.0;
+        dyn = rowBytes <= 512 &&
+              (batches == 1 || (batches < 0 && rowBytes == 512 && perItem >= batch_min_phases * NGl));
+    }
+    // static phases (no batches): the item's pieces placed so that its waves end together
+    // (balance_pieces; items with kept MFMA tiles keep the longest-first order, whose shortest
+    // pieces sit with the tile waves)
+    if (!dyn && piece_balance == 1) {
+        const u32 G = rowBytes >= 2048 ? 16 : rowBytes >= 1024 ? 8 : 4;  // sddmm.hip RowGeom
+        par_for(items.size(), [&](unsigned, size_t i0, size_t i1) {
+            for (size_t i = i0; i < i1; ++i)
+                if (items[i].y == items[i].z) balance_pieces(ipc[i], NT, G, piece_weight);
+        });
+    }
     std::vector<size_t> poff(items.size() + 1, 0);
     for (size_t i = 0; i < items.size(); ++i) poff[i + 1] = poff[i] + ipc[i].size();
     std::vector<uint2> pieces(poff.back());
@@ -2274,19 +2350,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         L.outPacked = true;
     }
     lap("staged");
-    // dynamic piece batches (Plan::batches; kernels for rows of <= 512 B): after its first batch
-    // of 64 / G pieces a wave takes the next from an LDS counter, which balances the waves of
-    // items with several pieces per row-group. Measured (profiles/r05bt, forced on against off):
-    // 512-byte rows with 2.4 / 6.5 / 6.8 pieces per row-group (mycielskian14 K = 128, C3, C4
-    // x0.5) -4.5 / -2.4 / -2.2 %, C2's 1.4 +5 %; 128- and 256-byte rows (mycielskian15 K = 32,
-    // Trefethen K = 64: little work per entry behind each counter round trip) +2 to +8 %. Auto:
-    // 512-byte rows from batch_min_phases pieces per row-group
-    {
-        const u32 NGl = NT / 4;  // row-groups (G = 4 for rows of <= 512 B)
-        const double perItem = L.nWorkItems ? static_cast<double>(pieces.size()) / L.nWorkItems : 0.0;
-        L.dynBatches = rowBytes <= 512 &&
-                       (batches == 1 || (batches < 0 && rowBytes == 512 && perItem >= batch_min_phases * NGl));
-    }
+    L.dynBatches = dyn;  // (decided with the piece order above)
     BSMR_CHECK(L.items.upload(items.data(), std::max<size_t>(items.size(), 1), s));
     BSMR_CHECK(L.itemEnd.upload(ends.data(), std::max<size_t>(ends.size(), 1), s));
     BSMR_CHECK(L.pieces.upload(pieces.data(), std::max<size_t>(pieces.size(), 1), s));

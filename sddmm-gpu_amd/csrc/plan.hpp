@@ -118,6 +118,10 @@ struct Plan {
     // row-group on average
     int batches = -1;
     double batch_min_phases = 2.0;
+    // static piece order of row-block items without dynamic batches (plan.hip balance_pieces;
+    // bsmr_tuning.piece_balance): 1 = runs dealt to the least-loaded wave, 0 = longest first in
+    // position order
+    int piece_balance = 0;
     float filter_ms = 0.f;
 
     // input

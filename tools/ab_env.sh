@@ -8,6 +8,10 @@ mkdir -p "$OUT"
 for c in $CFGS; do
     case "$c" in
         C2) ARGS="--workload nips_like --K 128 --dtype f32" ;;
+        C2k32) ARGS="--workload nips_like --K 32 --dtype f32" ;;
+        C2k64) ARGS="--workload nips_like --K 64 --dtype f32" ;;
+        C2k256) ARGS="--workload nips_like --K 256 --dtype f32" ;;
+        C2k512) ARGS="--workload nips_like --K 512 --dtype f32" ;;
         C3) ARGS="--workload cop20k_like --K 256 --dtype f16" ;;
         C4) ARGS="--workload reddit_like --scale 0.5 --K 128 --dtype f32" ;;
         C4x1) ARGS="--workload reddit_like --scale 1.0 --K 128 --dtype f32" ;;
@@ -20,6 +24,8 @@ for c in $CFGS; do
         M16k512) ARGS="--workload mycielskian16 --K 512 --alpha 0.5 --delta 0.7" ;;
         T64) ARGS="--workload Trefethen_20000 --K 64 --alpha 0.1 --delta 0.5" ;;
         T128) ARGS="--workload Trefethen_20000 --K 128 --alpha 0.1 --delta 0.5" ;;
+        M15k32) ARGS="--workload mycielskian15 --K 32 --alpha 0.9 --delta 0.1" ;;
+        M15k64) ARGS="--workload mycielskian15 --K 64 --alpha 0.3 --delta 0.1" ;;
     esac
     for v in $VALS; do
         sets=""; for V in ${VAR//,/ }; do sets="$sets $V=$v"; done
