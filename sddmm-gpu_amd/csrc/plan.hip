@@ -1815,33 +1815,39 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         // column weight: its entries, plus (item_sched) piece_weight per column-run piece it
         // heads, so the XCDs' ranges carry equal modeled cost rather than equal entry counts
         // (mycielskian: the last XCD's range carried 10 % more piece work and ended 10 % later)
-        // (sums over 16 fixed chunks of row blocks, whatever the host's thread count, added in
-        // chunk order: the cuts are the same on every host even for a non-integral piece_weight,
-        // so every rank of a multi-GPU run derives the same layout)
-        constexpr u32 NCH = 16;
-        std::vector<std::vector<double>> cntT(NCH);
-        par_for(NCH, [&](unsigned, size_t c0, size_t c1) {
-            for (size_t ch = c0; ch < c1; ++ch) {
-                std::vector<double>& cnt = cntT[ch];
-                const size_t b0 = static_cast<size_t>(nRB) * ch / NCH, b1 = static_cast<size_t>(nRB) * (ch + 1) / NCH;
-                if (b0 == b1) continue;
-                cnt.assign(N + 1, 0.0);
-                for (size_t b = b0; b < b1; ++b) {
-                    const u32 lo = b ? std::max(rbEnd[b - 1], 0u) : 0u, hi = rbEnd[b];
-                    u32 run = 0;
-                    for (u32 i = lo; i < hi; ++i) {
-                        const u32 c = hmeta[i] & CM;
-                        const bool start = i == lo || c != (hmeta[i - 1] & CM) || run >= piece_max;
-                        run = start ? 1 : run + 1;
-                        cnt[c] += 1.0 + (item_cost_cuts && start ? piece_weight : 0.0);
+        // (integer counts per column — entries, and column-run starts = ceil(run / piece_max) per
+        // row block — then cnt = entries + piece_weight x starts: exact whatever the host's thread
+        // count, so every rank of a multi-GPU run derives the same layout. Each host thread takes a
+        // stripe of columns and finds its part of every row block's column-sorted entries by
+        // binary search: N + 1 counters in all, not one vector per row-block chunk)
+        std::vector<u32> ecount(N + 1, 0), scount(N + 1, 0);
+        const u32 NSTR = 64;
+        par_for(NSTR, [&](unsigned, size_t s0, size_t s1) {
+            for (size_t st = s0; st < s1; ++st) {
+                const u32 c0 = static_cast<u32>(static_cast<u64>(N) * st / NSTR);
+                const u32 c1 = static_cast<u32>(static_cast<u64>(N) * (st + 1) / NSTR);
+                if (c0 == c1) continue;
+                for (u32 b = 0; b < nRB; ++b) {
+                    const u32* lo = hmeta.data() + (b ? rbEnd[b - 1] : 0u);
+                    const u32* hi = hmeta.data() + rbEnd[b];
+                    const auto byCol = [](u32 m, u32 c) { return (m & CM) < c; };
+                    const u32* p = std::lower_bound(lo, hi, c0, byCol);
+                    const u32* q = std::lower_bound(p, hi, c1, byCol);
+                    for (const u32* i = p; i < q;) {
+                        const u32 c = *i & CM;
+                        const u32* j = i + 1;
+                        while (j < q && (*j & CM) == c) ++j;
+                        const u32 n = static_cast<u32>(j - i);
+                        ecount[c] += n;
+                        scount[c] += (n + piece_max - 1) / piece_max;
+                        i = j;
                     }
                 }
             }
         }, 1);
         std::vector<double> cnt(N + 1, 0.0);
-        for (const auto& ct : cntT)
-            if (!ct.empty())
-                for (u32 c = 0; c <= N; ++c) cnt[c] += ct[c];
+        for (u32 c = 0; c < N; ++c)
+            cnt[c] = static_cast<double>(ecount[c]) + (item_cost_cuts ? piece_weight * scount[c] : 0.0);
         double tot = 0;
         for (u32 c = 0; c < N; ++c) tot += cnt[c];
         double run = 0;
