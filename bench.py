@@ -113,22 +113,47 @@ def workload(args):
         f"C5: dlmc_like 2048^2 90% sparse {args.mask} mask (seed 7), bf16 A/B, fp32 accumulate")
 
 
+# the CPUs this process may run on, read at start-up (an OpenMP runtime started with
+# OMP_PROC_BIND would bind the main thread to one place, and sched_getaffinity of the main thread
+# would no longer show the process's share)
+AFFINITY = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+AFFINITY_CPUS = len(AFFINITY)
+
+
 def host_threads():
     """Host threads for the CPU legs (OMP_NUM_THREADS = nproc): OMP_NUM_THREADS
     when the environment sets it — a GPU box exports its CPU share there (16 per GPU) — else
-    every CPU this process may run on (its affinity mask), never more than that mask."""
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
-    return max(1, min(n, aff))
+    every CPU this process may run on (its start-up affinity mask), never more than that mask."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or AFFINITY_CPUS
+    return max(1, min(n, AFFINITY_CPUS))
+
+
+def close_cpus(threads):
+    """BASELINE.md §2's OMP_PROC_BIND=close for the CPU leg's `threads` OpenMP threads: one per
+    physical core where the affinity set lists SMT siblings (Linux numbers them core, core + cores),
+    in order — the CPUs the oracle pins its team to (orc_sddmm_cpu_rows_bound), so only this team is
+    bound whatever OpenMP runtime the process started first."""
+    cores = []
+    try:
+        sib = {}
+        for c in AFFINITY:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib[c] = f.read().strip()
+        seen = set()
+        for c in AFFINITY:
+            if sib[c] not in seen:
+                seen.add(sib[c])
+                cores.append(c)
+    except OSError:
+        cores = list(AFFINITY)
+    return (cores + [c for c in AFFINITY if c not in cores])[:max(1, threads)]
 
 
 def host_cpu_info(threads):
     """What the CPU leg ran on (core count, binding, CPU model)."""
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
-    return {"threads": threads, "nproc": os.cpu_count(), "affinity_cpus": aff,
+    return {"threads": threads, "nproc": os.cpu_count(), "affinity_cpus": AFFINITY_CPUS,
             "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
-            "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"),
-            "OMP_PLACES": os.environ.get("OMP_PLACES"), "model": cpu_model()}
+            "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "model": cpu_model()}
 
 
 def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200, max_budget_s=75.0):
@@ -232,8 +257,10 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
             break
     nnz_s = int(rp[row_end])
     P = np.empty(len(ci), np.float32)
-    med, times, ok = steady_runs(lambda: lib.orc_sddmm_cpu_rows(c.h, K, Af, Bf, P, 0, row_end,
-                                                                threads))
+    cpus = np.asarray(close_cpus(threads), np.int32)
+    pinned = []
+    med, times, ok = steady_runs(lambda: pinned.append(lib.orc_sddmm_cpu_rows_bound(
+        c.h, K, Af, Bf, P, 0, row_end, threads, cpus.ctypes.data, len(cpus))))
     nerr = O.check_data(P[:nnz_s], P_gpu[:nnz_s])
     model = cpu_model()
     full = "full workload" if row_end == M else f"rows [0, {row_end}) of {M}"
@@ -244,12 +271,13 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
         "kind": "port",
         "sample": f"{full} (nnz={nnz_s}, K={K}), median of the last 5 of {len(times)} runs "
                   f"({'within 5 %' if ok else 'time budget reached before 5 runs agreed within 5 %'}), "
-                  f"OpenMP over rows (oracle/oracle.cpp orc_sddmm_cpu_rows, OMP_PROC_BIND="
-                  f"{os.environ.get('OMP_PROC_BIND')}); cpu: {model}",
+                  f"OpenMP over rows, threads pinned close, one per core (oracle/oracle.cpp "
+                  f"orc_sddmm_cpu_rows_bound); cpu: {model}",
         "ms": round(med * 1e3, 3),
         "steady": ok,
         "runs_ms": [round(t * 1e3, 3) for t in times],
-        "host": host_cpu_info(threads),
+        "host": dict(host_cpu_info(threads), bind="close (explicit)", cpus=[int(x) for x in cpus],
+                     threads_pinned=min(pinned) if pinned else 0),
         "checkData_errors_vs_gpu": nerr,
     }
 
@@ -616,10 +644,6 @@ def self_launch(args):
 
 
 def main():
-    # the CPU legs run OpenMP threads bound close (set before any OpenMP runtime
-    # loads: torch's and the oracle's read them at start-up); a caller's own setting stays
-    os.environ.setdefault("OMP_PROC_BIND", "close")
-    os.environ.setdefault("OMP_PLACES", "cores")
     args = parse()
     from bsmr import dist as D
 

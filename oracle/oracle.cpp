@@ -23,6 +23,8 @@
 #include <vector>
 
 #include <omp.h>
+#include <pthread.h>
+#include <sched.h>
 
 namespace {
 
@@ -1024,6 +1026,41 @@ extern "C" void orc_sddmm_cpu_rows(const orc_csr* c, uint32_t K, const float* A,
             P[idx] = val;
         }
     }
+}
+
+// The same loop with its OpenMP team pinned "close" (BASELINE.md §2's OMP_PROC_BIND=close, done
+// here so that only this team is bound, whatever OpenMP runtime the host process started first):
+// thread t runs on cpus[t % ncpus] (the caller passes its affinity set in order); the calling
+// thread's own mask is restored afterwards. Returns the threads that took their CPU.
+extern "C" int orc_sddmm_cpu_rows_bound(const orc_csr* c, uint32_t K, const float* A, const float* B,
+                                        float* P, uint32_t row_begin, uint32_t row_end, int nthreads,
+                                        const int* cpus, int ncpus) {
+    cpu_set_t saved;
+    CPU_ZERO(&saved);
+    const bool have = pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) == 0;
+    int pinned = 0;
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : pinned)
+    {
+        if (cpus && ncpus > 0) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus[omp_get_thread_num() % ncpus], &one);
+            pinned += pthread_setaffinity_np(pthread_self(), sizeof(one), &one) == 0;
+        }
+#pragma omp for schedule(static)
+        for (long row = row_begin; row < static_cast<long>(row_end); ++row) {
+            const float* a = A + static_cast<size_t>(row) * K;
+            for (u32 idx = c->rowptr[row]; idx < c->rowptr[row + 1]; ++idx) {
+                const float* b = B + static_cast<size_t>(c->col[idx]) * K;
+                float val = 0.0f;
+                for (u32 k = 0; k < K; ++k) val += a[k] * b[k];
+                P[idx] = val;
+            }
+        }
+    }
+    if (have) pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
+    return pinned;
 }
 
 extern "C" void orc_sddmm_cpu(const orc_csr* c, uint32_t K, const float* A, const float* B,

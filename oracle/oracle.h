@@ -101,6 +101,11 @@ void orc_sddmm_cpu(const orc_csr* c, uint32_t K, const float* A, const float* B,
 /* same, but only the rows [row_begin,row_end) (bounded CPU-baseline samples) */
 void orc_sddmm_cpu_rows(const orc_csr* c, uint32_t K, const float* A, const float* B, float* P,
                         uint32_t row_begin, uint32_t row_end, int num_threads);
+/* the same with thread t pinned to cpus[t % ncpus] (OMP_PROC_BIND=close done explicitly); the
+ * caller's mask is restored; returns the number of threads pinned */
+int orc_sddmm_cpu_rows_bound(const orc_csr* c, uint32_t K, const float* A, const float* B, float* P,
+                             uint32_t row_begin, uint32_t row_end, int nthreads, const int* cpus,
+                             int ncpus);
 
 /* ---- checkData (checkData.hpp:14-79) ---- */
 int orc_check_one(float a, float b);

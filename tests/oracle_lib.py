@@ -77,6 +77,9 @@ def lib():
         L.orc_sddmm_cpu.argtypes = [C.c_void_p, C.c_uint32, _f32p, _f32p, _f32p, C.c_int]
         L.orc_sddmm_cpu_rows.argtypes = [C.c_void_p, C.c_uint32, _f32p, _f32p, _f32p,
                                          C.c_uint32, C.c_uint32, C.c_int]
+        L.orc_sddmm_cpu_rows_bound.restype = C.c_int
+        L.orc_sddmm_cpu_rows_bound.argtypes = [C.c_void_p, C.c_uint32, _f32p, _f32p, _f32p,
+                                               C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_int]
         L.orc_check_one.restype = C.c_int
         L.orc_check_one.argtypes = [C.c_float, C.c_float]
         L.orc_check_data.restype = C.c_uint64
