@@ -577,7 +577,8 @@ struct DenseTileLds {
     __device__ __forceinline__ void loadB(const RbArgs& a, const int k0, f32x4 (&bv)[CH]) const {
         const u32 g = __lane_id() >> 4;
         const bool cvalid = c < a.N;
-        const char* bcol = a.B + static_cast<size_t>(cvalid ? c : 0) * RBY;
+        // BSMR_DIAG & 8388608 (ablation only): every tile reads B column 0, so its gathers hit L2
+        const char* bcol = a.B + static_cast<size_t>(cvalid && !(a.diag & 8388608u) ? c : 0) * RBY;
 #pragma unroll
         for (int kk = 0; kk < CH; ++kk)
             bv[kk] = cvalid ? ld16(bcol + 16 * chunk(k0 + kk, g)) : f32x4{0, 0, 0, 0};

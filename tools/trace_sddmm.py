@@ -31,9 +31,10 @@ def main():
     ap.add_argument("--scale", type=float, default=None, help="reddit_like size factor")
     ap.add_argument("--waves-per-wg", type=int, default=16, help="NT / 64 of the traced launch")
     ap.add_argument("--mask", default=None, help="dlmc_like mask: uniform | block")
-    ap.add_argument("--cold", action="store_true",
+    ap.add_argument("--cold", nargs="?", const="write", default=None, choices=["write", "read"],
                     help="trace a launch right after a 512 MiB write (Infinity Cache evicted, as "
-                         "bench.py's cold leg)")
+                         "bench.py's cold leg), or after a 512 MiB read (--cold read: evicted, "
+                         "caches clean, as the cold leg's 'clean' figure)")
     args = ap.parse_args()
     os.environ["BSMR_DIAG"] = str(int(os.environ.get("BSMR_DIAG", "0")) | 32)
     import torch
@@ -61,6 +62,10 @@ def main():
     if args.cold:  # evict the MALL, then the traced launch
         flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
         flush.fill_(1)
+        if args.cold == "read":
+            sink = torch.empty((), dtype=torch.int64, device="cuda")
+            for _ in range(3):
+                sink.copy_(flush.sum(dtype=torch.int64))
         torch.cuda.synchronize()
         plan.sddmm(dA.data_ptr(), dB.data_ptr(), K, dP.data_ptr(), stream=s, dtype=code)
         torch.cuda.synchronize()
