@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define BSMR_ABI_VERSION 12 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
+#define BSMR_ABI_VERSION 13 /* 2: bsmr_plan_shard_dtype, layout stats; 3: 128-byte rows (5 sizes);
                               4: dense_sampled_tiles, rb_orig_rows; 5: row-stage export/import,
                               bsmr_sddmm_panels_local, host SDDMM + checkData; 6: bsmr_tuning in
                               the plan options (no environment reads in the library);
@@ -33,7 +33,9 @@ extern "C" {
                               11: bsmr_tuning.batches, stats rb_batches;
                               12: bsmr_tuning.ptile / ptile_tpi (panel-grouped fp16/bf16 tile
                               launch), piece_balance, stats ptile_items, bsmr_cost_cuts; removed the dropped experiments'
-                              knobs piece_order, seg_items, sweep* and stats rb_sweep */
+                              knobs piece_order, seg_items, sweep* and stats rb_sweep;
+                              13: bsmr_tuning.col_blocks (column-block launch of wide patterns),
+                              stats rb_col_blocks */
 
 typedef enum {
     BSMR_OK = 0,
@@ -155,6 +157,10 @@ typedef struct {
                                   their pieces so that the waves' phase costs even out (runs of
                                   the longest-first list dealt to the least-loaded wave) instead of
                                   longest first in position order; 0 never, 1 always, -1 = auto */
+    int32_t col_blocks;        /* BSMR_COL_BLOCKS: column-block launch (blocks of original columns,
+                                  B rows staged, A rows gathered per row run) for the whole plan: 0
+                                  never, 1 always, -1 = auto (N >= 2 M and fewer than 0.9 x the
+                                  pieces of the row-block layout) */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);
@@ -259,6 +265,8 @@ typedef struct {
     uint32_t rb_pairs;
     /* bit i set: row-block layout i (as rb_rows) deals its pieces in dynamic batches */
     uint32_t rb_batches;
+    /* bit i set: row-block layout i (as rb_rows) is the column-block launch (bsmr_tuning.col_blocks) */
+    uint32_t rb_col_blocks;
 } bsmr_plan_stats;
 
 int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* out);

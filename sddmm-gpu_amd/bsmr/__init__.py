@@ -50,7 +50,7 @@ class Tuning(C.Structure):
                 ("item_sched", C.c_int32), ("out_packed", C.c_int32),
                 ("cluster_filter", C.c_int32), ("pair_min_items", C.c_int32),
                 ("batches", C.c_int32), ("ptile", C.c_int32), ("ptile_tpi", C.c_int32),
-                ("piece_balance", C.c_int32)]
+                ("piece_balance", C.c_int32), ("col_blocks", C.c_int32)]
 
 
 # tuning field <- its debug environment variable (bsmr_tuning_from_env)
@@ -84,7 +84,7 @@ class PlanStats(C.Structure):
                 ("dense_sampled_tiles", C.c_uint32), ("rb_orig_rows", C.c_uint32),
                 ("ptile_items", C.c_uint32), ("cluster_filter_used", C.c_uint32),
                 ("cluster_filter_ms", C.c_float), ("rb_pairs", C.c_uint32),
-                ("rb_batches", C.c_uint32)]
+                ("rb_batches", C.c_uint32), ("rb_col_blocks", C.c_uint32)]
 
     def as_dict(self):
         d = {}
@@ -124,7 +124,7 @@ class RowStage(C.Structure):
         return cls.from_buffer_copy(np.ascontiguousarray(a, np.uint8).tobytes())
 
 
-ABI_VERSION = 12  # include/bsmr.h BSMR_ABI_VERSION
+ABI_VERSION = 13  # include/bsmr.h BSMR_ABI_VERSION
 
 # every symbol include/bsmr.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -249,7 +249,7 @@ def tuning_from_env(env=None):
         if v is None:
             continue
         if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "cluster_filter",
-                 "batches", "ptile", "piece_balance"):  # tri-state: "0" never, "1" always, else auto
+                 "batches", "ptile", "piece_balance", "col_blocks"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
         elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap"):
             out[f] = float(v)

@@ -40,6 +40,7 @@ extern "C" void bsmr_tuning_default(bsmr_tuning* t) {
     t->batches = -1;
     t->ptile = t->ptile_tpi = -1;
     t->piece_balance = -1;
+    t->col_blocks = -1;
 }
 
 extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
@@ -91,6 +92,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     get3("BSMR_PTILE", t->ptile);
     geti("BSMR_PTILE_TPI", t->ptile_tpi);
     get3("BSMR_PIECE_BALANCE", t->piece_balance);
+    get3("BSMR_COL_BLOCKS", t->col_blocks);
     return n;
 }
 
@@ -149,6 +151,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->ptile >= 0) p.ptile_mode = t->ptile ? 1 : 0;
         if (t->ptile_tpi >= 0) p.ptile_tpi = static_cast<u32>(std::min(64, t->ptile_tpi));
         if (t->piece_balance >= 0) p.piece_balance = t->piece_balance ? 1 : 0;
+        if (t->col_blocks >= 0) p.col_blocks = t->col_blocks ? 1 : 0;
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;
@@ -366,6 +369,7 @@ extern "C" int bsmr_plan_get_stats(const bsmr_plan* plan, bsmr_plan_stats* s) {
         s->rb_tiles[i] = L.rowBytes ? L.nTilesKept : 0;
         s->rb_work_items[i] = L.rowBytes ? L.nWorkItems : 0;
         if (L.rowBytes && L.orig) s->rb_orig_rows |= 1u << i;
+        if (L.rowBytes && L.cols) s->rb_col_blocks |= 1u << i;
         if (L.rowBytes && rb_uses_pairs(p, L)) s->rb_pairs |= 1u << i;
         if (L.rowBytes && L.dynBatches) s->rb_batches |= 1u << i;
     }
@@ -591,7 +595,7 @@ extern "C" int bsmr_plan_shard_rebalance(const bsmr_plan* plan, uint32_t K, int 
     }
     const Plan& p = plan->p;
     const Plan::RowBlockLayout* L = nullptr;
-    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
+    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L, true));
     if (!L || L->nRB == 0 || L->orig) {
         set_error("bsmr_plan_shard_rebalance: needs the row-block launch of the reordered plan");
         return BSMR_ERR_UNSUPPORTED;
@@ -612,7 +616,7 @@ extern "C" int bsmr_plan_shard_dtype(const bsmr_plan* plan, uint32_t K, int dtyp
     // item costs (entries, column-run pieces, tiles, staged rows), so each shard's own layout has
     // the same row blocks; otherwise the per-panel model of bsmr_shard_cuts
     const Plan::RowBlockLayout* L = nullptr;
-    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L));
+    BSMR_CHECK(whole_rb_layout(p, K, dtype, &L, true));
     if (L && L->nRB > 0 && !L->orig) {  // (original-order row blocks do not map to panels)
         BSMR_CHECK(bsmr_cost_cuts(L->rbCost.data(), L->nRB, L->RB / 16, p.P, world, nullptr, nullptr,
                                   cuts.data()));

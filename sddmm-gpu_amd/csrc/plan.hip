@@ -1288,6 +1288,24 @@ __global__ __launch_bounds__(256) void k_rb_keys_csr(const u32* __restrict__ row
     }
 }
 
+// column blocks: key = (col / RB) * M + row for every stored entry (thread per row); qOf = the
+// entry's column (its image row), rowOf = its row (the gathered A row)
+__global__ __launch_bounds__(256) void k_rb_keys_cols(const u32* __restrict__ rowptr,
+                                                      const u32* __restrict__ colidx, u32 M, u32 RB,
+                                                      unsigned long long* __restrict__ keys,
+                                                      u32* __restrict__ vals, u32* __restrict__ qOf,
+                                                      u32* __restrict__ rowOf) {
+    const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= M) return;
+    for (u32 e = rowptr[r]; e < rowptr[r + 1]; ++e) {
+        const u32 c = colidx[e];
+        keys[e] = static_cast<unsigned long long>(c / RB) * M + r;
+        vals[e] = e;
+        qOf[e] = c;
+        rowOf[e] = r;
+    }
+}
+
 // stored entries of tiles [t0, t0 + gridDim.x) (one 256-thread block per tile)
 __global__ __launch_bounds__(256) void k_tile_nnz(const u32* __restrict__ blockValues, u32 t0,
                                                   u32* __restrict__ cnt) {
@@ -1508,6 +1526,21 @@ std::vector<u32> apportion(const std::vector<double>& cost, u32 q, double cap = 
 }
 }  // namespace
 
+// a candidate layout the launch does not use: its device arrays freed (its counts stay)
+static void release_layout(Plan::RowBlockLayout& L) {
+    L.meta.release();
+    L.out.release();
+    L.items.release();
+    L.itemEnd.release();
+    L.pieces.release();
+    L.tileIds.release();
+    L.rowIds.release();
+    L.sortedPos.release();
+    L.itemEnt.release();
+    L.runs.release();
+    L.itemRuns.release();
+}
+
 std::shared_ptr<const Plan::RowBlockLayout> Plan::rowblock_layout(u32 rowBytes, bool half,
                                                                   u32 pa, u32 pb, int* err) const {
     *err = BSMR_OK;
@@ -1518,6 +1551,7 @@ std::shared_ptr<const Plan::RowBlockLayout> Plan::rowblock_layout(u32 rowBytes, 
         RowBlockLayout& L = rbl[slot];
         if (L.rowBytes != rowBytes || L.tileMin != tmin) {
             rb_use_orig[slot] = false;
+            rb_use_cols[slot] = false;
             *err = build_rowblock_layout(L, rowBytes, 0, P, tmin);
             if (*err != BSMR_OK) return nullptr;
             // sparse rows (the same < 64 entries per row rule as the row-block sizing): try
@@ -1533,15 +1567,20 @@ std::shared_ptr<const Plan::RowBlockLayout> Plan::rowblock_layout(u32 rowBytes, 
                 // (C3 cop20k-like: 1.03 M -> 0.80 M pieces, 109 -> 78 us)
                 const double c = L.nPieces + 16.0 * L.nTilesKept, co = Lo.nPieces;
                 rb_use_orig[slot] = orig_rows == 1 || co < 0.9 * c;
-                if (!rb_use_orig[slot]) {  // keep the decision, free the candidate
-                    Lo.meta.release();
-                    Lo.out.release();
-                    Lo.items.release();
-                    Lo.itemEnd.release();
-                    Lo.pieces.release();
-                    Lo.tileIds.release();
-                    Lo.rowIds.release();
-                }
+                if (!rb_use_orig[slot]) release_layout(Lo);  // keep the decision, free the candidate
+            }
+            // wide patterns (N >= 2 M): column blocks, B rows staged and A rows gathered (the
+            // roles swapped), when their pieces are below 0.9 x the chosen layout's (C2 nips-like
+            // 1,500 x 12,419: 93.5 K -> 78 K pieces, 10.3 -> 9.3 us; tools/transpose_ab.py)
+            rb_use_cols[slot] = false;
+            if (col_blocks == 1 || (col_blocks != 0 && static_cast<u64>(N) >= 2ull * M)) {
+                RowBlockLayout& Lc = rblc[slot];
+                *err = build_rowblock_layout(Lc, rowBytes, 0, P, tmin, false, true);
+                if (*err != BSMR_OK) return nullptr;
+                const RowBlockLayout& Lw = rb_use_orig[slot] ? rblo[slot] : L;
+                const double cw = Lw.nPieces + 16.0 * Lw.nTilesKept;
+                rb_use_cols[slot] = col_blocks == 1 || Lc.nPieces < 0.9 * cw;
+                if (!rb_use_cols[slot]) release_layout(Lc);
             }
         }
         return std::shared_ptr<const RowBlockLayout>(std::shared_ptr<void>(), &rb_whole(slot));
@@ -1622,16 +1661,22 @@ static void balance_pieces(std::vector<uint2>& pcs, u32 NT, u32 G, double w) {
 }
 
 int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
-                                bool orig) const {
+                                bool orig, bool cols) const {
     L.rowBytes = 0;
-    L.orig = orig;
+    L.orig = orig && !cols;
+    L.cols = cols;
+    orig = orig && !cols;
+    // whole: original-order blocks of rows (orig) or of columns (cols), every entry residual
+    const bool whole = orig || cols;
+    // the gathered index space: columns of S, or (column blocks) its rows
+    const u32 NS = cols ? M : N;
     hipStream_t s = stream;
-    if (N > (1u << 22)) {
-        set_error("row-block layout needs N <= 2^22");
+    if (NS > (1u << 22)) {
+        set_error(cols ? "column-block layout needs M <= 2^22" : "row-block layout needs N <= 2^22");
         return BSMR_ERR_UNSUPPORTED;
     }
-    if (orig && (pa != 0 || pb != P)) {
-        set_error("original-order row blocks cover the whole plan only");
+    if (whole && (pa != 0 || pb != P)) {
+        set_error("original-order row / column blocks cover the whole plan only");
         return BSMR_ERR_INVALID;
     }
     // BSMR_DIAG & 524288: section times of this build to stderr (host-side layout cost)
@@ -1643,14 +1688,14 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                      std::chrono::duration<double, std::milli>(t - lap_t).count());
         lap_t = t;
     };
-    const u32 qa = orig ? 0 : 16 * pa, qend = orig ? M : std::min(R, 16 * pb);
+    const u32 qa = whole ? 0 : 16 * pa, qend = orig ? M : cols ? N : std::min(R, 16 * pb);
     const u32 Rs = qend > qa ? qend - qa : 0;  // (reordered) rows of the range
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
         cus = 256;
-    const u32 ebase = orig ? 0 : h_sparseValueOffsets[pa];
+    const u32 ebase = whole ? 0 : h_sparseValueOffsets[pa];
     // residual entries of the range (original order: every stored entry)
-    const u32 n0 = orig ? nnz : h_sparseValueOffsets[pb] - ebase;
+    const u32 n0 = whole ? nnz : h_sparseValueOffsets[pb] - ebase;
     // staged output (results through LDS, written per item in CSR order) for large P
     const bool stagedWanted = out_staged == 1 || (out_staged == -1 && 4ull * nnz > out_staged_min);
     // staged-output budget by row size (item_sched): 1 KiB rows take an 80 KiB image (two
@@ -1674,7 +1719,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // (profiles/r04x); x1 keeps two 7.5 MiB ranges; a share that fits the L2 stays one range
     // (mycielskian16 K = 128, 3 MiB per XCD: 166 us against 181 us with two; profiles/r04zr)
     const bool staged512 = stagedWanted && item_cost_cuts && rowBytes == 512;
-    const double shareKb = static_cast<double>(N) * rowBytes / XCD_BUCKETS / 1024.0;
+    const double shareKb = static_cast<double>(NS) * rowBytes / XCD_BUCKETS / 1024.0;
     const u32 l2Kb = l2_range_user ? l2_range_kb
                      : staged512 ? (shareKb > 4096.0 ? std::min<u32>(8192u, static_cast<u32>(std::ceil(shareKb / 2)) + 1)
                                                      : 8192u)
@@ -1689,7 +1734,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         const size_t lds0 = static_cast<size_t>(RBr) * rowBytes;
         const u32 slots = static_cast<u32>(cus) * (lds0 > 80 * 1024 ? 1u : 2u);
         const u32 nRB0 = (Rs + RBr - 1) / std::max<u32>(RBr, 1);
-        if (Rs && n0 < 64ull * Rs && nRB0 > slots) {
+        // (column blocks keep the whole image: their point is long row runs per block)
+        if (cols) {
+        } else if (Rs && n0 < 64ull * Rs && nRB0 > slots) {
             const u32 rounds = (nRB0 + slots - 1) / slots;
             const u32 rb = (Rs + rounds * slots - 1) / (rounds * slots);
             RBr = std::min(RBr, std::max<u32>(16, (rb + 15) / 16 * 16));
@@ -1705,13 +1752,20 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
             else RBr = std::min(RBr, rb1);
         }
     }
-    if (Rs && n0 >= 64ull * Rs && !(diag & 32768)) {
+    if (Rs && (cols || n0 >= 64ull * Rs) && !(diag & 32768)) {
         // non-sparse rows: the same number of row blocks, of equal size (a multiple of 16), so
         // no short last block and every item stages the smallest image that count allows (C2
         // nips-like: 5 x 288 + 60 rows -> 5 x 256 + 220, 10.80 -> 10.63 us; BSMR_DIAG & 32768
         // keeps the LDS-budget size)
         const u32 nb0 = (Rs + RBr - 1) / RBr;
         RBr = std::min(RBr, std::max<u32>(16, ((Rs + nb0 - 1) / nb0 + 15) / 16 * 16));
+    }
+    // column blocks: the largest image the workgroup's LDS takes (fewer blocks, longer row runs:
+    // C2 nips-like 288 -> 304 columns, 78.7 K -> 75.8 K pieces)
+    // (staged output keeps its budget: the result slots live past the image)
+    if (cols && !rb_lds_user && !stagedWanted && Rs) {
+        const u32 rmax = rowblock_rows(rowBytes, 160, Rs), nb0 = (Rs + rmax - 1) / rmax;
+        RBr = std::min(rmax, std::max<u32>(16, ((Rs + nb0 - 1) / nb0 + 15) / 16 * 16));
     }
     if (rb_rows_force > 0)  // tuning: rows per block (a multiple of 16 within the LDS budget)
         RBr = std::min(rowblock_rows(rowBytes, 160, Rs),
@@ -1726,7 +1780,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     const u32 wgPerCU = NT == 1024 ? 1 : 2;
     const u32 perBucket = std::max<u32>(1, static_cast<u32>(cus) * wgPerCU / XCD_BUCKETS);
     // dense tiles of the range: kept (>= tileMin stored entries) or demoted to entries
-    const u32 T0 = h_blockOffsets[pa], nT = orig ? 0 : h_blockOffsets[pb] - T0;
+    const u32 T0 = h_blockOffsets[pa], nT = whole ? 0 : h_blockOffsets[pb] - T0;
     std::vector<u32> tcnt(nT, 0), doff(nT, NULLV), keptPos(nT + 1ull, 0), hkept;
     u32 nd = 0;
     if (nT && tileMin > 0) {
@@ -1757,7 +1811,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     std::vector<u32> rbEnd(nRB, 0), hmeta(n);
     if (n) {
         DevBuf<unsigned long long> keys, skeys;
-        DevBuf<u32> vals, order, qOf, dEnd, ddoff, dcol, dout;
+        DevBuf<u32> vals, order, qOf, dEnd, ddoff, dcol, dout, rowOf;
         BSMR_CHECK(keys.alloc(n));
         BSMR_CHECK(skeys.alloc(n));
         BSMR_CHECK(vals.alloc(n));
@@ -1767,7 +1821,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         BSMR_CHECK(dcol.alloc(std::max<u32>(nd, 1)));
         BSMR_CHECK(dout.alloc(std::max<u32>(nd, 1)));
         BSMR_HIP(hipMemsetAsync(dEnd.data(), 0, nRB * sizeof(u32), s));
-        if (orig)
+        if (cols) {
+            BSMR_CHECK(rowOf.alloc(n));
+            hipLaunchKernelGGL(k_rb_keys_cols, dim3(grid_for(M, 256)), dim3(256), 0, s, rowptr.data(),
+                               colidx.data(), M, RBr, keys.data(), vals.data(), qOf.data(), rowOf.data());
+        } else if (orig)
             hipLaunchKernelGGL(k_rb_keys_csr, dim3(grid_for(M, 256)), dim3(256), 0, s, rowptr.data(),
                                colidx.data(), M, RBr, N, keys.data(), vals.data(), qOf.data());
         else if (pb > pa)
@@ -1782,11 +1840,11 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         }
         BSMR_HIP(hipGetLastError());
         BSMR_CHECK(sort_pairs64(keys.data(), skeys.data(), vals.data(), order.data(), n,
-                                bits_for(static_cast<u64>(nRB) * N), tmp, s));
-        if (orig)  // vals = CSR positions: the output index is the entry itself
+                                bits_for(static_cast<u64>(nRB) * NS), tmp, s));
+        if (whole)  // vals = CSR positions: the output index is the entry itself
             hipLaunchKernelGGL(k_rb_gather_csr, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
-                               qOf.data(), colidx.data(), n, RBr, L.meta.data(), L.out.data(),
-                               dEnd.data());
+                               qOf.data(), cols ? rowOf.data() : colidx.data(), n, RBr, L.meta.data(),
+                               L.out.data(), dEnd.data());
         else
             hipLaunchKernelGGL(k_rb_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, order.data(),
                                qOf.data(), sparseColIdx.data() + ebase, sparseValues.data() + ebase,
@@ -1807,9 +1865,9 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     constexpr u32 CM = (1u << 22) - 1;
     const u32 rangeKb = l2Kb;
     const u32 m = std::max<u32>(1, static_cast<u32>(std::ceil(
-        static_cast<double>(N) * rowBytes / XCD_BUCKETS / (static_cast<double>(rangeKb) * 1024.0))));
+        static_cast<double>(NS) * rowBytes / XCD_BUCKETS / (static_cast<double>(rangeKb) * 1024.0))));
     const u32 NCR = XCD_BUCKETS * m;
-    std::vector<u32> cuts(NCR + 1, N);
+    std::vector<u32> cuts(NCR + 1, NS);
     cuts[0] = 0;
     {
         // column weight: its entries, plus (item_sched) piece_weight per column-run piece it
@@ -1820,12 +1878,12 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         // count, so every rank of a multi-GPU run derives the same layout. Each host thread takes a
         // stripe of columns and finds its part of every row block's column-sorted entries by
         // binary search: N + 1 counters in all, not one vector per row-block chunk)
-        std::vector<u32> ecount(N + 1, 0), scount(N + 1, 0);
+        std::vector<u32> ecount(NS + 1, 0), scount(NS + 1, 0);
         const u32 NSTR = 64;
         par_for(NSTR, [&](unsigned, size_t s0, size_t s1) {
             for (size_t st = s0; st < s1; ++st) {
-                const u32 c0 = static_cast<u32>(static_cast<u64>(N) * st / NSTR);
-                const u32 c1 = static_cast<u32>(static_cast<u64>(N) * (st + 1) / NSTR);
+                const u32 c0 = static_cast<u32>(static_cast<u64>(NS) * st / NSTR);
+                const u32 c1 = static_cast<u32>(static_cast<u64>(NS) * (st + 1) / NSTR);
                 if (c0 == c1) continue;
                 for (u32 b = 0; b < nRB; ++b) {
                     const u32* lo = hmeta.data() + (b ? rbEnd[b - 1] : 0u);
@@ -1845,18 +1903,18 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
                 }
             }
         }, 1);
-        std::vector<double> cnt(N + 1, 0.0);
-        for (u32 c = 0; c < N; ++c)
+        std::vector<double> cnt(NS + 1, 0.0);
+        for (u32 c = 0; c < NS; ++c)
             cnt[c] = static_cast<double>(ecount[c]) + (item_cost_cuts ? piece_weight * scount[c] : 0.0);
         double tot = 0;
-        for (u32 c = 0; c < N; ++c) tot += cnt[c];
+        for (u32 c = 0; c < NS; ++c) tot += cnt[c];
         double run = 0;
         u32 x = 1;
-        for (u32 c = 0; c < N && x < NCR; ++c) {
+        for (u32 c = 0; c < NS && x < NCR; ++c) {
             while (x < NCR && run >= tot * x / NCR) cuts[x++] = c;
             run += cnt[c];
         }
-        for (; x < NCR; ++x) cuts[x] = N;
+        for (; x < NCR; ++x) cuts[x] = NS;
     }
     lap("cuts");
     // segments (rb, range k): entries of rb in range k + 1/NCR of rb's tiles; cost = entries +
@@ -1870,8 +1928,8 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
         const u32 eb0 = b ? rbEnd[b - 1] : 0, eb1 = rbEnd[b];
         const u32 p0 = std::min(pa + b * (RBr / 16), pb), p1 = std::min(pa + (b + 1) * (RBr / 16), pb);
         // kept tiles of the row block: positions [t0, t0 + nt) of the kept list
-        const u32 t0 = orig ? 0 : keptPos[h_blockOffsets[p0] - T0];
-        const u32 nt = orig ? 0 : keptPos[h_blockOffsets[p1] - T0] - t0;
+        const u32 t0 = whole ? 0 : keptPos[h_blockOffsets[p0] - T0];
+        const u32 nt = whole ? 0 : keptPos[h_blockOffsets[p1] - T0] - t0;
         u32 lo = eb0;
         for (u32 k = 0; k < NCR; ++k) {
             const size_t i = static_cast<size_t>(b) * NCR + k;
@@ -1922,10 +1980,15 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     std::vector<char> split(nRB, 0);
     double splitTotal = 0;
     std::vector<u32> segX(XCD_BUCKETS, 0);  // non-empty split segments per XCD
+    // column blocks whose whole gathered operand (A) fits half an XCD's L2 (C2: 768 KiB): no
+    // block is split by range, so each block's items run on one XCD (contiguous eighths) and its
+    // B image comes into that L2 once — split by range, every XCD would pull every block's image
+    // from the Infinity Cache (8 x B per launch) to save gathers of an A that is L2-resident anyway
+    const bool colsLocal = cols && static_cast<u64>(NS) * rowBytes <= (2ull << 20) && !(diag & 4096);
     for (u32 b = 0; b < nRB; ++b) {
         for (u32 k = 0; k < NCR; ++k) cb[b] += cost[static_cast<size_t>(b) * NCR + k];
-        split[b] = cb[b] >= XCD_BUCKETS * target ||
-                   (m > 1 && piecesRB[b] >= static_cast<u64>(NCR) * RBr);
+        split[b] = !colsLocal && (cb[b] >= XCD_BUCKETS * target ||
+                                  (m > 1 && piecesRB[b] >= static_cast<u64>(NCR) * RBr));
         if (!split[b]) continue;
         splitTotal += cb[b];
         for (u32 k = 0; k < NCR; ++k)
@@ -2053,7 +2116,7 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     }
     {
         const size_t nsp = lists[spare].size();
-        const bool contig = orig && orig_contig && qSplit == 0;
+        const bool contig = whole && orig_contig && qSplit == 0;
         if (item_lpt && !contig && nsp) {
             // list scheduling: each XCD runs its list on perBucket slots, an item starting when a
             // slot frees (in list order). The XCD lists' split items are simulated first; then
@@ -2368,10 +2431,10 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     L.pa = pa;
     L.pb = pb;
     L.rowEnd = qend;
-    if (orig) {
-        std::vector<u32> ids(M);
-        for (u32 r = 0; r < M; ++r) ids[r] = r;
-        BSMR_CHECK(L.rowIds.upload(ids.data(), std::max<u32>(M, 1), s));
+    if (whole) {  // identity over the staged rows (S's rows, or for column blocks its columns)
+        std::vector<u32> ids(qend);
+        for (u32 r = 0; r < qend; ++r) ids[r] = r;
+        BSMR_CHECK(L.rowIds.upload(ids.data(), std::max<u32>(qend, 1), s));
         BSMR_HIP(hipStreamSynchronize(s));
     }
     lap("upload");

@@ -207,6 +207,12 @@ struct Plan {
         // row block b = original rows [b RB, (b + 1) RB), staged through rowIds (identity), every
         // entry residual; whole-plan launches only (shards cut reordered panels)
         bool orig = false;
+        // column blocks (wide patterns, Plan::col_blocks): the roles of A and B swapped — block b
+        // = original COLUMNS [b RB, (b + 1) RB), their B rows staged through rowIds (identity over
+        // N), and each piece a run of one A row (an original row of S) over the block's columns;
+        // the metadata's "column" is that row, the output the entry's CSR position. The launch
+        // passes B as the staged operand and A as the gathered one; whole-plan launches only
+        bool cols = false;
         DevBuf<u32> rowIds;
         // dynamic piece batches (k_sddmm_rb / k_sddmm_rb_pair<.., true>; Plan::batches)
         bool dynBatches = false;
@@ -221,6 +227,12 @@ struct Plan {
     mutable RowBlockLayout rblo[N_RB_LAYOUTS];
     mutable bool rb_use_orig[N_RB_LAYOUTS] = {};
     int orig_rows = -1;
+    // whole-plan column-block candidates (built for wide patterns, N >= 2 M) and whether the
+    // launch uses them: their pieces are below 0.9 x those of the layout chosen above.
+    // BSMR_COL_BLOCKS: 0 = never, 1 = always, else auto
+    mutable RowBlockLayout rblc[N_RB_LAYOUTS];
+    mutable bool rb_use_cols[N_RB_LAYOUTS] = {};
+    int col_blocks = -1;
     // BSMR_ORIG_CONTIG: unsplit original-order blocks dealt as contiguous eighths per XCD (1)
     // or to the shortest list (0); C3: 78.6 -> 76.8 us (profiles/r01s)
     int orig_contig = 1;
@@ -235,9 +247,11 @@ struct Plan {
     // shared: a caller keeps its layout alive while another thread's request evicts it
     mutable std::vector<std::shared_ptr<RowBlockLayout>> shard_rbl;
     int build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb, u32 tileMin,
-                              bool orig = false) const;
-    // the whole-plan layout a launch of this slot uses (rbl or rblo)
-    const RowBlockLayout& rb_whole(int slot) const { return rb_use_orig[slot] ? rblo[slot] : rbl[slot]; }
+                              bool orig = false, bool cols = false) const;
+    // the whole-plan layout a launch of this slot uses (rbl, rblo or rblc)
+    const RowBlockLayout& rb_whole(int slot) const {
+        return rb_use_cols[slot] ? rblc[slot] : rb_use_orig[slot] ? rblo[slot] : rbl[slot];
+    }
     // the (cached) layout for rows of rowBytes over panels [pa, pb) for fp32 (half = false) or
     // fp16/bf16 operands; null on error. Call with layout_mu held; the whole-plan layouts are
     // plan members (non-owning pointer), a shard layout is shared with the cache
@@ -301,7 +315,8 @@ struct Plan {
 };
 
 // the whole plan's row-block layout for (K, dtype) (sddmm.hip); *out = null for column-major
-int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out);
+int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out,
+                    bool reordered = false);
 // whether a full launch of layout L runs two items per workgroup (k_sddmm_rb_pair; sddmm.hip)
 bool rb_uses_pairs(const Plan& p, const Plan::RowBlockLayout& L);
 

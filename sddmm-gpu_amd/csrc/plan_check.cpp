@@ -492,7 +492,7 @@ private:
             BSMR_CHECK(L.runs.download(runs, s));
             BSMR_CHECK(L.itemRuns.download(itemRuns, s));
         }
-        if (L.orig) BSMR_CHECK(L.rowIds.download(rowIds, s));
+        if (L.orig || L.cols) BSMR_CHECK(L.rowIds.download(rowIds, s));
         items.resize(L.nItems);
         iend.resize(L.nItems);
         pieces.resize(L.nPieces);
@@ -505,7 +505,12 @@ private:
         if (staged && !L.outRuns && sortedPos.size() < nE) return layout_fail("staged positions"), BSMR_OK;
         if (!staged && !L.outPacked && out.size() < nE) return layout_fail("output positions"), BSMR_OK;
         const u32 nRB = L.nRB, RB = L.RB;
-        const u32 qbase = L.orig ? 0 : 16 * L.pa;
+        const u32 qbase = (L.orig || L.cols) ? 0 : 16 * L.pa;
+        // column blocks: the image rows are S's columns (identity over N) and a piece's
+        // "column" is a row of S; every check below then runs on (row, column) swapped back
+        const u32 nStream = L.cols ? h_.M : h_.N;
+        if ((L.orig || L.cols) && rowIds.size() < L.rowEnd)
+            return layout_fail("original-order row list shorter than the staged rows"), BSMR_OK;
         {
             // the workgroup's LDS (launch_rb: 160 KiB at 1024 threads, 80 KiB at 512) holds the
             // image and, for staged output, the largest item's result slots past it; rows of
@@ -579,7 +584,7 @@ private:
                 u32 seen = 0;
                 for (u32 k = pw; k < pe && err.empty(); ++k) {
                     const u32 e0 = pieces[k].x, c = pieces[k].y & CM22, len = (pieces[k].y >> 22) + 1;
-                    if (static_cast<u64>(e0) + len > nE || c >= h_.N ||
+                    if (static_cast<u64>(e0) + len > nE || c >= nStream ||
                         (staged && (e0 < ea || e0 + len > ea + ne))) {
                         err = fmt("item %zu piece %u: entries [%u, +%u) column %u", i, k, e0, len, c);
                         break;
@@ -590,7 +595,7 @@ private:
                             err = fmt("item %zu entry %u: local row %u", i, e, lr);
                             break;
                         }
-                        const u32 row = L.orig ? rowIds[base + lr] : h_.rows[base + lr];
+                        const u32 img = (L.orig || L.cols) ? rowIds[base + lr] : h_.rows[base + lr];
                         u32 pos;
                         if (staged) {
                             const u32 slot = m & CM22;
@@ -604,8 +609,9 @@ private:
                             }
                             pos = out[e];
                         }
-                        if (!entry_ok(row, c, pos)) {
-                            err = fmt("item %zu entry %u: row %u col %u -> position %u", i, e, row, c, pos);
+                        const u32 row = L.cols ? c : img, col = L.cols ? img : c;
+                        if (!entry_ok(row, col, pos)) {
+                            err = fmt("item %zu entry %u: row %u col %u -> position %u", i, e, row, col, pos);
                             break;
                         }
                         if (bump(&ehit[e])) {

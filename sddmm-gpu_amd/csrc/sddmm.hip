@@ -1542,12 +1542,15 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
         a.A = reinterpret_cast<const char*>(reinterpret_cast<uintptr_t>(dA) -
                                             static_cast<uintptr_t>(16ull * L.pa * L.rowBytes));
     a.B = static_cast<const char*>(dB);
+    // column blocks: B's rows are the staged image, A's the gathered rows (the kernel computes
+    // the same dot products with the operands' roles swapped)
+    if (L.cols) std::swap(a.A, a.B);
     a.P = dP;
-    a.rows = local ? p.iotaR.data() : L.orig ? L.rowIds.data() : p.rows.data();
+    a.rows = local ? p.iotaR.data() : (L.orig || L.cols) ? L.rowIds.data() : p.rows.data();
     a.row0 = local ? 16 * L.pa : 0;
     a.R = L.rowEnd;
-    a.qbase = L.orig ? 0 : 16 * L.pa;
-    a.N = p.N;
+    a.qbase = (L.orig || L.cols) ? 0 : 16 * L.pa;
+    a.N = L.cols ? p.M : p.N;
     a.RB = L.RB;
     a.items = L.items.data();
     a.itemEnd = L.itemEnd.data();
@@ -1585,8 +1588,8 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
         BSMR_CHECK(p.prepare_trace(static_cast<size_t>(L.nItems) * (L.NT / 64), s));
         a.trace = p.trace.data();
     }
-    a.bA = static_cast<unsigned long long>(p.M) * L.rowBytes;
-    a.bB = static_cast<unsigned long long>(p.N) * L.rowBytes;
+    a.bA = static_cast<unsigned long long>(L.cols ? p.N : p.M) * L.rowBytes;
+    a.bB = static_cast<unsigned long long>(L.cols ? p.M : p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
 #define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, L.dynBatches)
@@ -1655,13 +1658,16 @@ bool sddmm_uses_ptile(const Plan& p, u32 K, int dtype) { return use_ptile(p, K, 
 
 // the whole plan's row-block layout for (K, dtype), built on first use; *out = null when that
 // (K, dtype) runs the column-major launch
-int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out) {
+int whole_rb_layout(const Plan& p, u32 K, int dtype, const Plan::RowBlockLayout** out,
+                    bool reordered) {
     *out = nullptr;
     const int slot = rb_slot(p, K, dtype);
     if (slot < 0 || use_ptile(p, K, dtype)) return BSMR_OK;
     std::shared_ptr<const Plan::RowBlockLayout> L;  // the whole plan's: a plan member
     BSMR_CHECK(get_rb_layout(p, slot, dtype, 0, p.P, &L));
     *out = L.get();
+    // reordered: the reordered-row layout (always built first; panel shards cut its row blocks)
+    if (reordered && (L->orig || L->cols)) *out = &p.rbl[slot + (dtype != BSMR_F32 ? Plan::N_RB_SIZES : 0)];
     return BSMR_OK;
 }
 
@@ -1801,8 +1807,9 @@ extern "C" int bsmr_sddmm_panels_local(const bsmr_plan* plan, const void* dA_loc
     }
     std::shared_ptr<const Plan::RowBlockLayout> L;  // held until the launch is enqueued
     BSMR_CHECK(get_rb_layout(p, slot, dtype, p0, p1, &L));
-    if (L->orig)  // the whole range may have picked original-order row blocks: use the
-                  // reordered layout (always built first), whose rows follow the local A
+    if (L->orig || L->cols)  // the whole range may have picked original-order row blocks or
+                             // column blocks: use the reordered layout (always built first), whose
+                             // rows follow the local A
         L = std::shared_ptr<const Plan::RowBlockLayout>(
             std::shared_ptr<void>(), &p.rbl[slot + (dtype != BSMR_F32 ? Plan::N_RB_SIZES : 0)]);
     return launch_rb(p, *L, dA_local, dB, dP, dtype, 3, static_cast<hipStream_t>(stream), 1, true);

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in sorted(declared) if not hasattr(L, s)]
     assert not missing, missing
     assert declared == set(bsmr.EXPORTS), declared ^ set(bsmr.EXPORTS)
-    assert L.bsmr_abi_version() == bsmr.ABI_VERSION == 12
+    assert L.bsmr_abi_version() == bsmr.ABI_VERSION == 13
 
 
 def test_rocsparse_baseline_exports_every_header_symbol():

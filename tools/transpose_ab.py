@@ -37,6 +37,10 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--rb-rows", type=int, nargs="*", default=[128, 256, 304],
+                    help="forced rows per block of the S^T launch (besides its own rule, -1)")
+    ap.add_argument("--s-rb-rows", type=int, nargs="*", default=[],
+                    help="forced rows per block of extra S launches (original and BSMR row order)")
     args = ap.parse_args()
     import torch
 
@@ -50,10 +54,16 @@ def main():
     dB = torch.from_numpy(make_data(N * K)).to(dev)
     dP = torch.zeros(len(ci), dtype=torch.float32, device=dev)
     s = torch.cuda.current_stream(dev)
-    plans = {"S": (Plan(M, N, rp, ci, alpha=0.3, delta=0.3), dA, dB)}
+    plans = {"S": (Plan(M, N, rp, ci, alpha=0.3, delta=0.3), dA, dB),
+             "S_rows": (Plan(M, N, rp, ci, alpha=0.3, delta=0.3, tuning={"col_blocks": 0}), dA, dB)}
     for orig in (0, 1):
-        plans[f"ST_orig{orig}"] = (Plan(Mt, Nt, rpt, cit, alpha=0.3, delta=0.3,
-                                        tuning={"orig_rows": orig}), dB, dA)
+        for rbr in args.s_rb_rows:
+            plans[f"S_orig{orig}_rb{rbr}"] = (Plan(M, N, rp, ci, alpha=0.3, delta=0.3,
+                                                   tuning={"orig_rows": orig, "rb_rows": rbr}), dA, dB)
+    for orig in (0, 1):
+        for rbr in [-1] + args.rb_rows:
+            plans[f"ST_orig{orig}_rb{rbr}"] = (Plan(Mt, Nt, rpt, cit, alpha=0.3, delta=0.3,
+                                                    tuning={"orig_rows": orig, "rb_rows": rbr}), dB, dA)
 
     def timed(name):
         plan, X, Y = plans[name]
