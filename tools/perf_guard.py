@@ -33,7 +33,9 @@ sys.path.insert(0, os.path.join(ROOT, "sddmm-gpu_amd"))
 
 # (alpha, delta) of the best test-mode setting per (matrix, K) on MI355X
 # (profiles/r04zv/ss_compare_8f76aec.json)
-SS_BEST_FILE = os.path.join(ROOT, "profiles", "r04zv", "ss_compare_8f76aec.json")
+# (a copy of profiles/r04zv/ss_compare_8f76aec.json outside the round directories, which GPU runs
+# do not receive: .gpurunignore)
+SS_BEST_FILE = os.path.join(ROOT, "profiles", "perf_guard_ss_points.json")
 SS = ["Trefethen_20000", "Trefethen_20000b", "mycielskian14", "mycielskian15", "mycielskian16"]
 
 
