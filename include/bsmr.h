@@ -159,8 +159,8 @@ typedef struct {
                                   longest first in position order; 0 never, 1 always, -1 = auto */
     int32_t col_blocks;        /* BSMR_COL_BLOCKS: column-block launch (blocks of original columns,
                                   B rows staged, A rows gathered per row run) for the whole plan: 0
-                                  never, 1 always, -1 = auto (N >= 2 M and fewer than 0.9 x the
-                                  pieces of the row-block layout) */
+                                  never, 1 always, 2 = wide patterns (N >= 2 M) with fewer than 0.9 x
+                                  the pieces of the row-block layout; -1 = 0 */
 } bsmr_tuning;
 
 void bsmr_tuning_default(bsmr_tuning* t);

@@ -249,7 +249,7 @@ def tuning_from_env(env=None):
         if v is None:
             continue
         if f in ("orig_rows", "out_staged", "stage_nt", "item_sched", "out_packed", "cluster_filter",
-                 "batches", "ptile", "piece_balance", "col_blocks"):  # tri-state: "0" never, "1" always, else auto
+                 "batches", "ptile", "piece_balance"):  # tri-state: "0" never, "1" always, else auto
             out[f] = 0 if v.startswith("0") else 1 if v.startswith("1") else -1
         elif f in ("piece_weight", "shard_piece_weight", "dense_min", "item_cap"):
             out[f] = float(v)

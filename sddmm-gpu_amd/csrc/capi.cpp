@@ -92,7 +92,7 @@ extern "C" int bsmr_tuning_from_env(bsmr_tuning* t) {
     get3("BSMR_PTILE", t->ptile);
     geti("BSMR_PTILE_TPI", t->ptile_tpi);
     get3("BSMR_PIECE_BALANCE", t->piece_balance);
-    get3("BSMR_COL_BLOCKS", t->col_blocks);
+    geti("BSMR_COL_BLOCKS", t->col_blocks);
     return n;
 }
 
@@ -151,7 +151,7 @@ int init_plan(Plan& p, const bsmr_plan_options& o) {
         if (t->ptile >= 0) p.ptile_mode = t->ptile ? 1 : 0;
         if (t->ptile_tpi >= 0) p.ptile_tpi = static_cast<u32>(std::min(64, t->ptile_tpi));
         if (t->piece_balance >= 0) p.piece_balance = t->piece_balance ? 1 : 0;
-        if (t->col_blocks >= 0) p.col_blocks = t->col_blocks ? 1 : 0;
+        if (t->col_blocks >= 0) p.col_blocks = std::min(2, t->col_blocks);
         if (t->l2_range_kb >= 0) {
             p.l2_range_kb = static_cast<u32>(std::max(64, t->l2_range_kb));
             p.l2_range_user = true;

@@ -1569,11 +1569,11 @@ std::shared_ptr<const Plan::RowBlockLayout> Plan::rowblock_layout(u32 rowBytes, 
                 rb_use_orig[slot] = orig_rows == 1 || co < 0.9 * c;
                 if (!rb_use_orig[slot]) release_layout(Lo);  // keep the decision, free the candidate
             }
-            // wide patterns (N >= 2 M): column blocks, B rows staged and A rows gathered (the
-            // roles swapped), when their pieces are below 0.9 x the chosen layout's (C2 nips-like
-            // 1,500 x 12,419: 93.5 K -> 78 K pieces, 10.3 -> 9.3 us; tools/transpose_ab.py)
+            // column blocks, B rows staged and A rows gathered (the roles swapped): always (1),
+            // or (2) for wide patterns (N >= 2 M) when their pieces are below 0.9 x the chosen
+            // layout's (C2 nips-like 1,500 x 12,419: 93.5 K -> 75.8 K pieces, the same time)
             rb_use_cols[slot] = false;
-            if (col_blocks == 1 || (col_blocks != 0 && static_cast<u64>(N) >= 2ull * M)) {
+            if (col_blocks == 1 || (col_blocks == 2 && static_cast<u64>(N) >= 2ull * M)) {
                 RowBlockLayout& Lc = rblc[slot];
                 *err = build_rowblock_layout(Lc, rowBytes, 0, P, tmin, false, true);
                 if (*err != BSMR_OK) return nullptr;
@@ -1764,7 +1764,10 @@ int Plan::build_rowblock_layout(RowBlockLayout& L, u32 rowBytes, u32 pa, u32 pb,
     // C2 nips-like 288 -> 304 columns, 78.7 K -> 75.8 K pieces)
     // (staged output keeps its budget: the result slots live past the image)
     if (cols && !rb_lds_user && !stagedWanted && Rs) {
-        const u32 rmax = rowblock_rows(rowBytes, 160, Rs), nb0 = (Rs + rmax - 1) / rmax;
+        // (batches never: no piece-batch counter to keep free, so the image may fill the LDS)
+        const u32 rfull = std::min<u32>(std::min<u32>(160u * 1024u / rowBytes / 16 * 16, 1024),
+                                        std::max<u32>((Rs + 15) / 16 * 16, 16));
+        const u32 rmax = batches == 0 ? rfull : rowblock_rows(rowBytes, 160, Rs), nb0 = (Rs + rmax - 1) / rmax;
         RBr = std::min(rmax, std::max<u32>(16, ((Rs + nb0 - 1) / nb0 + 15) / 16 * 16));
     }
     if (rb_rows_force > 0)  // tuning: rows per block (a multiple of 16 within the LDS budget)

@@ -227,12 +227,13 @@ struct Plan {
     mutable RowBlockLayout rblo[N_RB_LAYOUTS];
     mutable bool rb_use_orig[N_RB_LAYOUTS] = {};
     int orig_rows = -1;
-    // whole-plan column-block candidates (built for wide patterns, N >= 2 M) and whether the
-    // launch uses them: their pieces are below 0.9 x those of the layout chosen above.
-    // BSMR_COL_BLOCKS: 0 = never, 1 = always, else auto
+    // whole-plan column-block layouts and whether the launch uses them. BSMR_COL_BLOCKS: 0 =
+    // never (default: on C2, the one wide BASELINE pattern, 19 % fewer pieces measured 1 % slower
+    // at steady state and 0-4 % faster from a standing start), 1 = always, 2 = for
+    // wide patterns (N >= 2 M) whose column-block pieces are below 0.9 x the chosen layout's
     mutable RowBlockLayout rblc[N_RB_LAYOUTS];
     mutable bool rb_use_cols[N_RB_LAYOUTS] = {};
-    int col_blocks = -1;
+    int col_blocks = 0;
     // BSMR_ORIG_CONTIG: unsplit original-order blocks dealt as contiguous eighths per XCD (1)
     // or to the shortest list (0); C3: 78.6 -> 76.8 us (profiles/r01s)
     int orig_contig = 1;

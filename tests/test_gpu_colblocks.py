@@ -30,17 +30,17 @@ def _check(plan, M, N, rp, ci, K, dtype=F32):
     return P
 
 
-def test_c2_takes_column_blocks_by_default():
-    """BASELINE.json C2 (nips-like 1,500 x 12,419, fp32 K = 128): the auto rule picks column blocks
-    (N >= 2 M, pieces below 0.9 x the row-block layout's), P matches the oracle and the layout
-    check passes entry by entry."""
+def test_c2_piece_rule_takes_column_blocks():
+    """BASELINE.json C2 (nips-like 1,500 x 12,419, fp32 K = 128): the piece rule (col_blocks = 2)
+    picks column blocks (N >= 2 M, pieces below 0.9 x the row-block layout's), P matches the
+    oracle and the layout check passes entry by entry; the default keeps row blocks."""
     M, N, rp, ci = synth.nips_like()
-    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
+    plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, tuning={"col_blocks": 2})
     _check(plan, M, N, rp, ci, 128)
     st = plan.stats()
     assert st["rb_col_blocks"] & (1 << SLOT[128]), st
     assert plan.check(128, F32, verbose=False) == (True, "")
-    off = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE, tuning={"col_blocks": 0})
+    off = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, free_mem_bytes=FREE)
     _check(off, M, N, rp, ci, 128)
     assert off.stats()["rb_col_blocks"] == 0
     assert st["rb_pieces"][SLOT[128]] < 0.9 * off.stats()["rb_pieces"][SLOT[128]]
