@@ -7,6 +7,9 @@ rows (S's columns) in LDS and gathers A rows per column-run piece. On a wide pat
 (offline count, 256-row / 256-column blocks: 95.5 K pieces against 83.6 K). This times both —
 the plan of S (the product launch) and a plan of S^T with A and B swapped (its P in S^T's CSR
 order, so only the time is compared) — alternating, 200 launches per timing, HIP events.
+Caveat (round 6): the variants run in a fixed order each round, so the first one also carries the
+device's ramp from a standing start; tools/layout_ab.py (graphs, many rounds) is the A/B to trust —
+on it the column-block layout (col_blocks = 1) times the same as the row-block one.
 
     python3 tools/transpose_ab.py [--reps 3] [--orig -1|0|1]
 """
