@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true",
                     help="time the steps as stream launches only (default: the K timed steps "
                          "captured into one HIP graph and replayed; both are reported)")
+    ap.add_argument("--sustained", action="store_true",
+                    help="also time the K-step graph after ~40 ms of back-to-back replays (the "
+                         "busy-device figure, timing.sustained_*; information only)")
     ap.add_argument("--cold-steps", type=int, default=20,
                     help="steps timed after evicting the 256 MiB Infinity Cache (0 = skip)")
     return ap.parse_args()
@@ -889,8 +892,10 @@ def main_single(args):
             timing["method"] = "stream_launches"
     if graph_ms is not None:
         ms_per_step = graph_ms
+    if graph_ms is not None and args.sustained:
         # the same K steps on a busy device (information only: the line's value stays the
-        # standing-start figure above)
+        # standing-start figure above; opt-in, so a rocprofv3 summary of the default command
+        # averages the same launches as the value)
         sus_ms, sus_reps = sustained_time(lambda h: plan.sddmm(dA.data_ptr(), dB.data_ptr(), K,
                                                                dP.data_ptr(), stream=h, dtype=dtype),
                                           args.steps, dev)

@@ -8,6 +8,7 @@
 #   bench:<cfg>             bench.py line of one config (C1 C2 C3 C4 C4x1 C5u C5b C2k32 C2k512)
 #   quick:<cfg>             the same without the CPU / vendor legs and PMC passes
 #   pmc:<cfg>               the same without the CPU / vendor legs, with the in-run PMC traffic
+#   sustained:<cfg>         quick, plus the busy-device time (--sustained: timing.sustained_*)
 #   graph:<cfg>             quick, plus the timed steps replayed from one HIP graph (graph_replay)
 #   rocprof:<cfg>           rocprofv3 --kernel-trace --stats of that config's bench (every traced
 #                           launch a timed step)
@@ -67,6 +68,7 @@ run_step() {
             fi ;;
         bench) timeout -k 10 900 python3 bench.py $(cfg_args "$arg") > "$OUT/bench_$arg.json" 2> "$OUT/bench_$arg.err" ;;
         quick) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") $QUICK > "$OUT/quick_$arg.json" 2> "$OUT/quick_$arg.err" ;;
+        sustained) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") $QUICK --sustained > "$OUT/sustained_$arg.json" 2> "$OUT/sustained_$arg.err" ;;
         graph) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") $QUICK --graph > "$OUT/graph_$arg.json" 2> "$OUT/graph_$arg.err" ;;
         pmc) timeout -k 10 600 python3 bench.py $(cfg_args "$arg") --no-cpu-baseline --no-vendor --pmc on > "$OUT/pmc_$arg.json" 2> "$OUT/pmc_$arg.err" ;;
         rocprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$arg" -o run -- \
