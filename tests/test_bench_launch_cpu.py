@@ -65,3 +65,17 @@ def test_child_failure_propagates():
                         "--warmup", "0", "--no-cpu-baseline", "--no-vendor", "--pmc", "off"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode != 0
+
+
+def test_cpu_leg_pins_one_thread_per_core_in_the_affinity_set():
+    """BASELINE.md §2's OMP_PROC_BIND=close for the CPU leg: bench.close_cpus lists CPUs of the
+    start-up affinity set, distinct, physical cores (one SMT sibling each) first, in order."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    aff = set(bench.AFFINITY)
+    for n in (1, 2, len(aff), len(aff) + 3):
+        cpus = bench.close_cpus(n)
+        assert len(cpus) == min(max(n, 1), len(aff))
+        assert len(set(cpus)) == len(cpus) and set(cpus) <= aff
+    assert 1 <= bench.host_threads() <= len(aff)

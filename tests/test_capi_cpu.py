@@ -149,3 +149,27 @@ def test_tuning_env_parser_matches_python_mapping(monkeypatch):
     assert from_c == {k: v for k, v in from_py.items() if k != "orig_rows"}
     with pytest.raises(bsmr.BsmrError):
         bsmr._tuning_struct({"no_such_knob": 1})
+
+
+def test_tuning_defaults_and_struct_size():
+    """bsmr_tuning_default fills exactly the ctypes mirror of the (ABI 13) tuning struct, every
+    knob at its "keep the measured default" value; col_blocks (the column-block launch) is -1."""
+    n = ctypes.sizeof(bsmr.Tuning)
+    buf = (ctypes.c_uint8 * (n + 32))(*([0xAB] * (n + 32)))
+    bsmr.lib().bsmr_tuning_default(ctypes.cast(buf, ctypes.POINTER(bsmr.Tuning)))
+    assert bytes(buf[n:]) == b"\xab" * 32
+    t = bsmr.Tuning.from_buffer(buf)
+    assert t.diag == 0 and t.col_blocks == -1 and t.piece_balance == -1 and t.ptile == -1
+    assert [f for f, _ in bsmr.Tuning._fields_][-1] == "col_blocks"
+    assert [f for f, _ in bsmr.PlanStats._fields_][-1] == "rb_col_blocks"
+
+
+def test_col_blocks_env_values(monkeypatch):
+    """BSMR_COL_BLOCKS takes 0 / 1 / 2 (never, always, the wide-pattern piece rule) through both
+    the library's parser and the Python mapping."""
+    for k in bsmr.TUNING_ENV.values():
+        monkeypatch.delenv(k, raising=False)
+    for v in ("0", "1", "2"):
+        monkeypatch.setenv("BSMR_COL_BLOCKS", v)
+        assert bsmr.tuning_from_env() == {"col_blocks": int(v)}
+        assert bsmr.tuning_from_env({"BSMR_COL_BLOCKS": v}) == {"col_blocks": int(v)}
