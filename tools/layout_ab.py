@@ -55,7 +55,7 @@ def main():
     dB = torch.from_numpy(make_data(N * K)).to(dev).to(tdt)
     dP = torch.zeros(len(ci), dtype=torch.float32, device=dev)
     gs = torch.cuda.Stream(dev)
-    graphs, stats = {}, {}
+    graphs, stats, mism, ref_P = {}, {}, {}, None
     for v in args.variant:
         name, tun = parse_variant(v)
         plan = Plan(M, N, rp, ci, alpha=0.3, delta=0.3, tuning=tun)
@@ -70,6 +70,14 @@ def main():
             g.replay()
         gs.synchronize()
         graphs[name] = (g, plan)
+        Pv = dP.cpu().numpy().copy()
+        if ref_P is None:
+            ref_P = Pv
+        else:  # the same products: checkData's rule against the first variant
+            import numpy as np
+            d = np.abs(Pv - ref_P)
+            bad = (d >= 1e-5) & (d / np.maximum(np.maximum(np.abs(Pv), np.abs(ref_P)), 1e-3) >= 1e-3)
+            mism[name] = int(bad.sum())
         st = plan.stats()
         stats[name] = {"tuning": tun, "rb_rows": st["rb_rows"], "rb_pieces": st["rb_pieces"],
                        "rb_col_blocks": st["rb_col_blocks"]}
@@ -100,7 +108,8 @@ def main():
             gs.synchronize()
             res[name].append(round(e0.elapsed_time(e1) * 1e3 / args.steps, 3))
     out = {"config": args.config, "K": K, "steps": args.steps, "rounds": args.rounds,
-           "median_us": {k: statistics.median(v) for k, v in res.items()}, "us": res, "layouts": stats}
+           "median_us": {k: statistics.median(v) for k, v in res.items()}, "us": res, "layouts": stats,
+           "checkData_errors_vs_first": mism}
     print(json.dumps(out))
 
 
