@@ -1139,7 +1139,10 @@ __device__ __forceinline__ bool rb_item(const RbArgs& a, char* As, const u32 idx
 // (This single-item kernel keeps its own body rather than calling rb_item: the shared form
 // measured 3 % slower on C2, 10.70 vs 10.46 us on one box, with the same instruction count; the
 // pair kernel below uses rb_item.)
-template <int DT, int RBY, int NT, bool DYN>
+// LITE: the form the C2-like launches take — no kept MFMA tiles, one store per entry (no staged
+// output), default staging policy, phase-0 B after the barrier, no trace or ablations (launch_rb
+// picks it only then): the same instructions on that path, without the code of the others
+template <int DT, int RBY, int NT, bool DYN, bool LITE = false>
 __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char AsB[];
     char* As = AsB;
@@ -1153,7 +1156,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     constexpr u32 NW = NT / 64;               // waves per workgroup
     constexpr u32 NG = NT / G;                // residual row-groups
     constexpr u32 TC = DenseTileLds<DT, RBY>::CH;
-    const unsigned long long t0 = rtime(a.trace);
+    const unsigned long long t0 = LITE ? 0ull : rtime(a.trace);
     uint4 it = a.items[blockIdx.x];
     // all four fields in SGPRs before the padding test: the compiler otherwise loads .x (the row
     // block) in a second, dependent round trip after the test
@@ -1168,8 +1171,8 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     // every wave takes (at most) one dense tile and its row-groups one residual piece each per
     // phase; the first tile and the phase-0 pieces (B operand, metadata) are issued before the
     // staging loads so all of it is in flight together
-    const u32 ntile = (a.mode & 1) ? it.z - it.y : 0u;
-    const u32 np = (a.mode & 2) ? pend - it.w : 0u;
+    const u32 ntile = !LITE && (a.mode & 1) ? it.z - it.y : 0u;
+    const u32 np = LITE || (a.mode & 2) ? pend - it.w : 0u;
     const u32 gr = tid / G;
     u32 rot[NC];  // residual: byte offset of the G-chunk group the lane visits at step f
 #pragma unroll
@@ -1221,14 +1224,15 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
     const u32 tw = NW - 1 - w;
     Piece<RBY> pc;
     pc.len = 0;
-    if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
+    if constexpr (!LITE)
+        if (tw < ntile) dt.meta(a, a.tileIds[it.y + tw], q0);
     if (gr < np) load_piece_desc<RBY>(a, it.w + gr, pc);
     // staged output by runs: this lane's run descriptor (run w + NW * lane of the item), loaded
     // in the item's last piece phase, where the next-phase prefetch registers are free, so the
     // store pass waits for nothing but the LDS slots
     uint2 myrun = make_uint2(0u, 0u), irun = make_uint2(0u, 0u);
     auto load_runs = [&]() {
-        if (a.runs && a.outLds) {
+        if (!LITE && a.runs && a.outLds) {
             irun = a.itemRuns[blockIdx.x];
             irun.x = __builtin_amdgcn_readfirstlane(irun.x);
             irun.y = __builtin_amdgcn_readfirstlane(irun.y);
@@ -1267,14 +1271,14 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             }
         }
     };
-    if (a.stageNt)
+    if (!LITE && a.stageNt)
         stage(std::integral_constant<int, 2>{});
     else
         stage(std::integral_constant<int, 0>{});
     // the phase-0 B columns and entry metadata: issued right behind the LDS-DMAs (so the
     // barrier's wait covers them too), or with lateB after the barrier (the barrier then waits
     // for the staging alone and the waves pay one load round trip before their first piece)
-    if (!a.lateB) {
+    if (!LITE && !a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
         if (tw < ntile) dt.loadB(a, 0, tb);
     }
@@ -1285,17 +1289,19 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
         if (tid == 0) *reinterpret_cast<u32*>(As + (NT == 1024 ? 160u : 80u) * 1024u - 4u) = 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (a.lateB) {
+    if (LITE || a.lateB) {
         if (gr < np) load_piece_body<RBY>(a, sub, rot, pre, pc);
-        if (tw < ntile) dt.loadB(a, 0, tb);
+        if constexpr (!LITE)
+            if (tw < ntile) dt.loadB(a, 0, tb);
     }
-    const unsigned long long tm = rtime(a.trace);
-    if (a.diag & 8) {  // staging only
+    const unsigned long long tm = LITE ? 0ull : rtime(a.trace);
+    if (!LITE && (a.diag & 8)) {  // staging only
         trace_wave(a.trace, blockIdx.x * NW + w, t0, tm);
         return;
     }
-    if (tw < ntile) dt.run(a, As, tb);
-    const unsigned long long td = rtime(a.trace);
+    if constexpr (!LITE)
+        if (tw < ntile) dt.run(a, As, tb);
+    const unsigned long long td = LITE ? 0ull : rtime(a.trace);
     // later phases (items with more pieces than row-groups, e.g. short column runs): phase ph
     // runs the column window [ph NG, (ph + 1) NG) of the item's pieces (longest first inside;
     // Plan::build_rowblock_layout), dealt forwards in even and backwards in odd phases so a wave
@@ -1327,6 +1333,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb(RbArgs a) {
             if (pc.len) residual_piece<DT, RBY>(a, As, pc, sub, rot, pre);
         }
     }
+    if constexpr (LITE) return;
     for (u32 t = it.y + tw + NW; t < it.z; t += NW) {  // tiles beyond one per wave
         dt.load(a, a.tileIds[t], q0, tb);
         dt.run(a, As, tb);
@@ -1402,7 +1409,7 @@ __global__ __launch_bounds__(NT, 4) void k_sddmm_rb_pair(RbArgs a) {
 }
 
 template <int DT, int RBY>
-void (*pick_rb(const u32 NT, const bool pairs, const bool dyn))(RbArgs) {
+void (*pick_rb(const u32 NT, const bool pairs, const bool dyn, const bool lite))(RbArgs) {
     // (dynamic batches: rows of <= 512 B, RowBlockLayout::dynBatches)
     if constexpr (RBY >= 256) {  // (launch_rb enables pairs from 512-byte rows)
         if (pairs) {
@@ -1413,6 +1420,7 @@ void (*pick_rb(const u32 NT, const bool pairs, const bool dyn))(RbArgs) {
     }
     if constexpr (RBY <= 512)
         if (dyn) return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true> : k_sddmm_rb<DT, RBY, 512, true>;
+    if (lite) return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false, true> : k_sddmm_rb<DT, RBY, 512, false, true>;
     return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false> : k_sddmm_rb<DT, RBY, 512, false>;
 }
 
@@ -1592,7 +1600,11 @@ int launch_rb(const Plan& p, const Plan::RowBlockLayout& L, const void* dA, cons
     a.bB = static_cast<unsigned long long>(L.cols ? p.M : p.N) * L.rowBytes;
     a.bP = p.nnz;
     void (*fn)(RbArgs) = nullptr;
-#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, L.dynBatches)
+    // the LITE single-item kernel: the whole launch (mode 3), no kept tiles, direct stores, default
+    // staging policy, late B, no trace or ablation bits (BSMR_DIAG & 33554432 keeps the full form
+    // for A/B)
+    const bool lite = mode == 3 && L.nTilesKept == 0 && !a.outLds && !a.stageNt && a.lateB && p.diag == 0;
+#define BSMR_RB(DT, RBY) pick_rb<DT, RBY>(L.NT, a.pairs != 0, L.dynBatches, lite)
 #define BSMR_RB2(DT)                                                                   \
     (L.rowBytes == 128    ? BSMR_RB(DT, 128)                                              \
      : L.rowBytes == 256  ? BSMR_RB(DT, 256)                                              \
