@@ -1419,7 +1419,10 @@ void (*pick_rb(const u32 NT, const bool pairs, const bool dyn, const bool lite))
         }
     }
     if constexpr (RBY <= 512)
-        if (dyn) return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true> : k_sddmm_rb<DT, RBY, 512, true>;
+        if (dyn) {
+            if (lite) return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true, true> : k_sddmm_rb<DT, RBY, 512, true, true>;
+            return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, true> : k_sddmm_rb<DT, RBY, 512, true>;
+        }
     if (lite) return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false, true> : k_sddmm_rb<DT, RBY, 512, false, true>;
     return NT == 1024 ? k_sddmm_rb<DT, RBY, 1024, false> : k_sddmm_rb<DT, RBY, 512, false>;
 }
