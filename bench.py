@@ -159,14 +159,17 @@ def host_cpu_info(threads):
             "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "model": cpu_model()}
 
 
-def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200, max_budget_s=75.0):
-    """Time fn() until the last `window` runs agree within `tol` (max / min - 1), or the time
-    budget ends (at least `window` runs either way). Returns (median of the last window in s,
-    every run's seconds, whether the window converged). The first runs of a host loop on a fresh
-    box fall steadily (page faults, frequency ramp: 3.1 -> 0.9 ms over 50 runs of C1 in round 3),
-    so a median over all runs mixes the warm-up drift into the figure. Long runs (C4 x1: ~3 s at
-    16 threads) get room for 20 of them: budget max(budget_s, 20 x the first run), at most
-    max_budget_s."""
+def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200, max_budget_s=75.0,
+                drift_tol=0.03):
+    """Time fn() until steady, or until the time budget ends (at least `window` runs either way).
+    Steady: the last `window` runs agree within `tol` (max / min - 1), or — runs that scatter
+    more than that on a shared host (C4 x1: 2.6-3.1 s per run at 16 threads) — the median of the
+    last window is within `drift_tol` of the median of the window before it (no drift left, only
+    run-to-run noise). Returns (median of the last window in s, every run's seconds, the criterion
+    that held: "window", "no drift" or None). The first runs of a host loop on a fresh box fall
+    steadily (page faults, frequency ramp: 3.1 -> 0.9 ms over 50 runs of C1 in round 3), so a
+    median over all runs mixes the warm-up drift into the figure. Long runs (C4 x1: ~3 s) get room
+    for 20 of them: budget max(budget_s, 20 x the first run), at most max_budget_s."""
     times = []
     t0 = time.perf_counter()
     fn()
@@ -177,7 +180,13 @@ def steady_runs(fn, budget_s=20.0, window=5, tol=0.05, max_runs=200, max_budget_
         fn()
         times.append(time.perf_counter() - t0)
         last = times[-window:]
-        ok = len(times) >= window and max(last) <= (1.0 + tol) * min(last)
+        ok = None
+        if len(times) >= window and max(last) <= (1.0 + tol) * min(last):
+            ok = "window"
+        elif len(times) >= 2 * window:
+            m1, m0 = statistics.median(last), statistics.median(times[-2 * window:-window])
+            if abs(m1 - m0) <= drift_tol * m1:
+                ok = "no drift"
         if ok or len(times) >= max_runs or (len(times) >= window and time.perf_counter() > t_end):
             return statistics.median(last), times, ok
 
@@ -314,11 +323,12 @@ def cpu_baseline(M, N, rp, ci, K, A, B, P_gpu):
         "cores": threads,
         "kind": "port",
         "sample": f"{full} (nnz={nnz_s}, K={K}), median of the last 5 of {len(times)} runs "
-                  f"({'within 5 %' if ok else 'time budget reached before 5 runs agreed within 5 %'}), "
+                  f"({'within 5 %' if ok == 'window' else 'its median within 3 % of the 5 before (no drift; runs scatter more than 5 % on this host)' if ok else 'time budget reached before the runs were steady'}), "
                   f"OpenMP over rows, threads pinned close, one per core (oracle/oracle.cpp "
                   f"orc_sddmm_cpu_rows_bound); cpu: {model}",
         "ms": round(med * 1e3, 3),
-        "steady": ok,
+        "steady": bool(ok),
+        "steady_criterion": ok,
         "runs_ms": [round(t * 1e3, 3) for t in times],
         "host": dict(host_cpu_info(threads), bind="close (explicit)", cpus=[int(x) for x in cpus],
                      threads_pinned=min(pinned) if pinned else 0),
@@ -808,8 +818,8 @@ def main_c1(args):
         "cpu": {"cores": threads, "model": cpu_model(), "host": host_cpu_info(threads),
                 "kind": "product host SDDMM "
                 "(csrc/host_check.cpp, host.cpp:45-76 loop order, no FMA contraction)",
-                "runs_ms": [round(t * 1e3, 4) for t in times], "steady": steady,
-                "rule": "runs until the last 5 agree within 5 % (budget max(20 s, 20 runs)); "
+                "runs_ms": [round(t * 1e3, 4) for t in times], "steady": bool(steady), "steady_criterion": steady,
+                "rule": "runs until the last 5 agree within 5 % or their median is within 3 % of the 5 before (budget max(20 s, 20 runs)); "
                         "value = median of the last 5"},
         "checkData_errors_cpu_vs_gpu": nerr,
         "gpu_same_workload": {"value": round(flops / (gpu_ms * 1e-3) / 1e9, 2),
