@@ -528,9 +528,15 @@ def kernel_name(st, st_after, K, dtype, layout):
         pair = (4 * st["nnz"] > (8 << 20) and rby >= 512 and st_after["rb_items"][i] >= 4096
                 and not st_after["rb_tiles"][i])
         name = "k_sddmm_rb_pair" if pair else "k_sddmm_rb"
-        return (f"{name}<{dtype},{rby},{nt}> (row-block LDS layout, {rby}-byte rows, {rows} "
+        # template arguments as rocprofv3 prints them: <dtype, row bytes, threads, dynamic piece
+        # batches, lean single-item form (no kept tiles, direct stores; sddmm.hip launch_rb)>
+        dyn = bool(st_after.get("rb_batches", 0) & (1 << i))
+        lite = not pair and 4 * st["nnz"] <= (8 << 20) and not st_after["rb_tiles"][i]
+        targs = f"{dtype},{rby},{nt},{str(dyn).lower()}" + ("" if pair else f",{str(lite).lower()}")
+        return (f"{name}<{targs}> (row-block LDS layout, {rby}-byte rows, {rows} "
                 f"rows per block: residual entries; {tiles}"
-                f"{'; staged output by runs, two items per workgroup' if pair else ''})"), rby
+                f"{'; staged output by runs, two items per workgroup' if pair else ''}"
+                f"{'; lean single-item kernel' if lite else ''})"), rby
     if dtype == F32:
         return f"k_sddmm_f32<{K}> (column-major slots: dense-tile MFMA + residual)", rby
     return f"k_sddmm_half<{'f16' if dtype == 1 else 'bf16'}> (dense-tile MFMA + residual)", rby
